@@ -1,0 +1,168 @@
+/* lrt.h — C-ABI of the MI355X path tracer (liblrt_hip.so).
+ *
+ * Drop-in boundary for the reference's src/cpu renderer API
+ * (Sefaice/LearnRayTracing src/cpu/parallel.h:6-8):
+ *
+ *     void InitializeTest();                                         -> lrt_initialize
+ *     void ShutdownTest();                                           -> lrt_shutdown
+ *     void DrawTest(float time, int frameCount, int screenWidth,
+ *                   int screenHeight, float* backbuffer, int& outRayCount);
+ *                                                                    -> lrt_draw_test
+ *
+ * plus the extended entry points the multi-GPU / benchmark callers need
+ * (runtime scene and camera, device-resident progressive buffer, S samples per
+ * call, D bounces, row-block-cyclic sharding, 64-bit ray counts).
+ *
+ * Plain types and pointers only. Every function returns LRT_OK (0) or a negative
+ * LRT_E_* code; lrt_last_error() describes the last failure of the calling thread.
+ * Not re-entrant per process (like the reference's global scheduler, parallel.cpp:229).
+ */
+#ifndef LRT_H
+#define LRT_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LRT_OK 0
+#define LRT_E_INVALID (-1) /* bad argument (sizes, pointers, scene contents)        */
+#define LRT_E_HIP (-2)     /* a HIP runtime call failed                              */
+#define LRT_E_STATE (-3)   /* lrt_initialize() not called / already shut down        */
+#define LRT_E_NOMEM (-4)   /* device allocation failed                               */
+
+/* Material::Type, parallel.cpp:31 */
+#define LRT_LAMBERT 0
+#define LRT_METAL 1
+#define LRT_DIELECTRIC 2
+
+/* Reference kMaxDepth (parallel.cpp:12): lrt_draw_test allows this many scatter events. */
+#define LRT_REFERENCE_MAX_DEPTH 20
+/* Largest scene the device path accepts (spheres + materials are staged per workgroup). */
+#define LRT_MAX_SPHERES 4096
+
+/* float3, maths.h:10-61 (12 bytes, no padding) */
+typedef struct lrt_float3 { float x, y, z; } lrt_float3;
+
+/* Sphere, maths.h:156-163 (16 bytes) */
+typedef struct lrt_sphere { lrt_float3 center; float radius; } lrt_sphere;
+
+/* Material, parallel.cpp:29-37 (36 bytes: type @0, albedo @4, emissive @16,
+ * roughness @28, ri @32). type is the enum's int value. */
+typedef struct lrt_material {
+    int32_t type;
+    lrt_float3 albedo;
+    lrt_float3 emissive;
+    float roughness;
+    float ri;
+} lrt_material;
+
+/* Camera, maths.h:176-225 (88 bytes: the member order of the reference). */
+typedef struct lrt_camera {
+    lrt_float3 origin;
+    lrt_float3 a, u, r;
+    lrt_float3 lowerLeftCorner;
+    lrt_float3 horizontalVec;
+    lrt_float3 verticalVec;
+    float lensRadius;
+} lrt_camera;
+
+/* One render call (the extended form of DrawTest, parallel.cpp:297-323).
+ *
+ * The image is width x height; pixel (x, y) has row 0 at the bottom (v grows with y,
+ * maths.h:198,214). The call renders the column window [x0, x0 + x_count) of
+ * row_count LOCAL rows; local row ly maps to the global row
+ *     y = y0 + (ly / row_block) * row_block * row_period + row_phase * row_block + ly % row_block
+ * (row_period = 1, row_phase = 0 gives the contiguous rows y0 .. y0 + row_count - 1;
+ *  row_period = G, row_phase = g gives GPU g's share of a row-block-cyclic split).
+ * For each pixel it runs samples frame0 .. frame0 + frames - 1 in order; sample f
+ * uses the per-pixel XorShift32 stream seeded with
+ *     ((uint32)(x * 1973 + y * 9277 + f * 26699)) | 1
+ * and is blended into the buffer with the reference's progressive lerp
+ * (parallel.cpp:262,280-286): rgb = prev * (f / (f + 1)) + col * (1 - f / (f + 1)).
+ * max_depth is the number of scatter events a path may take (the reference's
+ * kMaxDepth = 20; "8 bounces" = 8). */
+typedef struct lrt_render_desc {
+    lrt_camera camera;
+    int32_t width, height;
+    int32_t x0, x_count;
+    int32_t y0, row_count;
+    int32_t row_block, row_period, row_phase;
+    int32_t frame0, frames;
+    int32_t max_depth;
+    int32_t flags; /* LRT_F_* */
+} lrt_render_desc;
+
+#define LRT_F_NONE 0
+#define LRT_F_SCENE_GLOBAL 1 /* read the scene from global memory instead of LDS staging */
+
+/* ---- the reference API (parallel.h:6-8) ---------------------------------- */
+
+/* InitializeTest (parallel.cpp:231-235): binds the calling thread's current HIP device,
+ * creates the stream, uploads the reference's default 9-sphere scene (parallel.cpp:15-51). */
+int lrt_initialize(void);
+
+/* ShutdownTest (parallel.cpp:237-240): frees every device resource. */
+int lrt_shutdown(void);
+
+/* DrawTest (parallel.cpp:297-323): one progressive frame of the current scene with
+ * DrawTest's camera (parallel.cpp:299-307) and kMaxDepth 20 into a caller-owned host
+ * buffer of screenWidth*screenHeight*4 floats (RGBA stride, alpha untouched), blocking.
+ * `time` is accepted and unused, as in the reference. */
+int lrt_draw_test(float time, int frameCount, int screenWidth, int screenHeight,
+                  float* backbuffer, int* outRayCount);
+
+/* ---- extended API -------------------------------------------------------- */
+
+const char* lrt_last_error(void);
+/* Library version string ("lrt-mi355x <semver> gfx950"). */
+const char* lrt_version(void);
+
+/* Camera constructor (maths.h:183-202). */
+int lrt_camera_make(lrt_float3 lookFrom, lrt_float3 lookAt, lrt_float3 vup, float vfov,
+                    float aspect, float aperture, float focusDist, lrt_camera* out);
+/* DrawTest's camera for a width x height image (parallel.cpp:299-307). */
+int lrt_camera_default(int width, int height, lrt_camera* out);
+
+/* Replace the scene (the reference's s_Spheres / s_SphereMats, parallel.cpp:15-51).
+ * 1 <= count <= LRT_MAX_SPHERES; material types must be 0..2. Emissive spheres are
+ * those with any emissive channel > 0 (parallel.cpp:96). */
+int lrt_set_scene(const lrt_sphere* spheres, const lrt_material* materials, int count);
+/* Copy the reference's default scene (9 spheres) into caller arrays of >= 9 entries. */
+int lrt_default_scene(lrt_sphere* spheres, lrt_material* materials, int capacity, int* count);
+
+/* Render into a DEVICE buffer of row_count * x_count RGBA float quads (row-major,
+ * local rows), adding the counted rays into *d_rays (device uint64, caller-zeroed).
+ * Asynchronous on `stream` (a hipStream_t; NULL = the library's stream). */
+int lrt_render_device(const lrt_render_desc* desc, float* d_backbuffer,
+                      unsigned long long* d_rays, void* stream);
+
+/* Same on a HOST buffer: H2D of prev, render, D2H, blocking. *out_rays = counted rays. */
+int lrt_render_host(const lrt_render_desc* desc, float* backbuffer, long long* out_rays);
+
+/* Number of local rows GPU `phase` owns in a row-block-cyclic split of `height` rows
+ * into blocks of row_block rows dealt over `period` GPUs. */
+int lrt_shard_rows(int height, int row_block, int period, int phase);
+
+/* Frame assembly after a gather: src holds `period` shard buffers of max_rows rows each
+ * (max_rows = lrt_shard_rows(height, row_block, period, 0)), shard g at
+ * src + g * max_rows * width * 4; dst receives the full width x height RGBA image.
+ * Device pointers, asynchronous on stream. */
+int lrt_unshard_rows(const float* d_src, float* d_dst, int width, int height, int row_block,
+                     int period, void* stream);
+
+/* Present step (main.cpp:109-141 LinearToSRGB + BGRA8 pack, GDI blit removed):
+ * d_rgba (width*height*4 floats) -> d_bgra (width*height uint32, b | g<<8 | r<<16). */
+int lrt_present_bgra8(const float* d_rgba, uint32_t* d_bgra, int width, int height, void* stream);
+
+/* ---- diagnostics (libm restatement, lrt_libm.h) --------------------------- */
+/* kind 0: sinf, 1: cosf, 2: powf(x, 5), 3: powf(x, 0.416666667f) (LinearToSRGB).
+ * Host evaluation of the restatement. */
+int lrt_libm_eval_host(int kind, const float* in, float* out, long long n);
+/* Device evaluation of the same restatement (device pointers, blocking). */
+int lrt_libm_eval_device(int kind, const float* d_in, float* d_out, long long n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LRT_H */

@@ -1,0 +1,131 @@
+"""ctypes binding of liblrt_hip.so (the C-ABI declared in include/lrt.h).
+
+The library is the product: HIP kernels for gfx950 plus the C-ABI shim. There is no
+CPU fallback anywhere in this package -- if the library is missing or fails to load,
+`lib()` raises LrtError.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblrt_hip.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "lrt.h")
+
+LRT_OK = 0
+LRT_E_INVALID = -1
+LRT_E_HIP = -2
+LRT_E_STATE = -3
+LRT_E_NOMEM = -4
+
+LAMBERT, METAL, DIELECTRIC = 0, 1, 2          # parallel.cpp:31
+REFERENCE_MAX_DEPTH = 20                      # parallel.cpp:12
+MAX_SPHERES = 4096
+F_SCENE_GLOBAL = 1
+
+
+class LrtError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"lrt error {code}: {msg}")
+        self.code = code
+
+
+class Float3(ctypes.Structure):               # maths.h:10-61
+    _fields_ = [("x", ctypes.c_float), ("y", ctypes.c_float), ("z", ctypes.c_float)]
+
+    def tolist(self):
+        return [self.x, self.y, self.z]
+
+
+class Sphere(ctypes.Structure):               # maths.h:156-163
+    _fields_ = [("center", Float3), ("radius", ctypes.c_float)]
+
+
+class Material(ctypes.Structure):             # parallel.cpp:29-37
+    _fields_ = [("type", ctypes.c_int32), ("albedo", Float3), ("emissive", Float3),
+                ("roughness", ctypes.c_float), ("ri", ctypes.c_float)]
+
+
+class Camera(ctypes.Structure):               # maths.h:176-225
+    _fields_ = [("origin", Float3), ("a", Float3), ("u", Float3), ("r", Float3),
+                ("lowerLeftCorner", Float3), ("horizontalVec", Float3),
+                ("verticalVec", Float3), ("lensRadius", ctypes.c_float)]
+
+    def to22(self):
+        out = []
+        for name in ("origin", "a", "u", "r", "lowerLeftCorner", "horizontalVec", "verticalVec"):
+            out += getattr(self, name).tolist()
+        return out + [self.lensRadius]
+
+
+class RenderDesc(ctypes.Structure):           # lrt_render_desc
+    _fields_ = [("camera", Camera),
+                ("width", ctypes.c_int32), ("height", ctypes.c_int32),
+                ("x0", ctypes.c_int32), ("x_count", ctypes.c_int32),
+                ("y0", ctypes.c_int32), ("row_count", ctypes.c_int32),
+                ("row_block", ctypes.c_int32), ("row_period", ctypes.c_int32),
+                ("row_phase", ctypes.c_int32),
+                ("frame0", ctypes.c_int32), ("frames", ctypes.c_int32),
+                ("max_depth", ctypes.c_int32), ("flags", ctypes.c_int32)]
+
+
+_c = ctypes
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+# name -> (restype, argtypes); must cover every function include/lrt.h declares
+SIGNATURES = {
+    "lrt_initialize": (_i, []),
+    "lrt_shutdown": (_i, []),
+    "lrt_draw_test": (_i, [_c.c_float, _i, _i, _i, _vp, _c.POINTER(_i)]),
+    "lrt_last_error": (_c.c_char_p, []),
+    "lrt_version": (_c.c_char_p, []),
+    "lrt_camera_make": (_i, [Float3, Float3, Float3, _c.c_float, _c.c_float, _c.c_float,
+                             _c.c_float, _c.POINTER(Camera)]),
+    "lrt_camera_default": (_i, [_i, _i, _c.POINTER(Camera)]),
+    "lrt_set_scene": (_i, [_c.POINTER(Sphere), _c.POINTER(Material), _i]),
+    "lrt_default_scene": (_i, [_c.POINTER(Sphere), _c.POINTER(Material), _i, _c.POINTER(_i)]),
+    "lrt_render_device": (_i, [_c.POINTER(RenderDesc), _vp, _vp, _vp]),
+    "lrt_render_host": (_i, [_c.POINTER(RenderDesc), _vp, _c.POINTER(_c.c_longlong)]),
+    "lrt_shard_rows": (_i, [_i, _i, _i, _i]),
+    "lrt_unshard_rows": (_i, [_vp, _vp, _i, _i, _i, _i, _vp]),
+    "lrt_present_bgra8": (_i, [_vp, _vp, _i, _i, _vp]),
+    "lrt_libm_eval_host": (_i, [_i, _vp, _vp, _c.c_longlong]),
+    "lrt_libm_eval_device": (_i, [_i, _vp, _vp, _c.c_longlong]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load liblrt_hip.so once; raise LrtError if it is not built."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise LrtError(LRT_E_STATE, f"{LIB_PATH} is missing: run __graft_entry__.build() "
+                                            "(make -C learnraytracing_amd/csrc)")
+            try:
+                handle = ctypes.CDLL(LIB_PATH)
+            except OSError as e:   # pragma: no cover - depends on the box
+                raise LrtError(LRT_E_STATE, f"cannot load {LIB_PATH}: {e}") from e
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(handle, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = handle
+        return _lib
+
+
+def check(rc: int) -> int:
+    """Raise LrtError for a negative LRT_E_* return code."""
+    if rc < 0:
+        msg = lib().lrt_last_error().decode(errors="replace")
+        raise LrtError(rc, msg)
+    return rc
+
+
+def f3(x, y, z) -> Float3:
+    return Float3(float(x), float(y), float(z))

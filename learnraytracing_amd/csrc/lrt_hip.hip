@@ -1,0 +1,528 @@
+// liblrt_hip.so — the MI355X path tracer behind the C-ABI of include/lrt.h.
+//
+// One work-item per pixel (TraceRowJob's per-pixel body, parallel.cpp:270-286), all
+// S samples of a pixel inside the work-item (so the progressive lerp sequence of S
+// DrawTest calls is reproduced bit for bit from the buffer's prev value), 16x16-pixel
+// workgroups made of four 8x8 wave tiles (neighbouring pixels take similar paths),
+// the sphere table staged into LDS once per workgroup, RGBA written back with one
+// 16-byte store per pixel, rays counted per lane and reduced once per wave.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "lrt.h"
+#include "lrt_trace.h"
+
+#define LRT_VERSION_STRING "lrt-mi355x 0.1.0 gfx950"
+
+namespace lrt {
+
+constexpr int kTileX = 16;
+constexpr int kTileY = 16;
+constexpr int kBlock = kTileX * kTileY;  // 4 waves
+constexpr int kMaxDepthSupported = 64;
+constexpr int kLdsSphereLimit = 4096;     // 64 KiB of float4
+
+struct KernelArgs {
+    CameraDev cam;
+    const float4* sph;
+    const float4* mats;
+    const int* lights;
+    int count, nlights;
+    int width, height;
+    int x0, xc, y0, rows;
+    int rb, rp, rph;
+    int frame0, frames, maxDepth;
+    float4* out;
+    unsigned long long* rays;
+};
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+template <int MAXD, bool kLds>
+__global__ __launch_bounds__(kBlock) void trace_kernel(const KernelArgs a) {
+    extern __shared__ float4 s_sph[];
+    const int tid = threadIdx.x;
+    if (kLds) {
+        for (int i = tid; i < a.count; i += kBlock) s_sph[i] = a.sph[i];
+        __syncthreads();
+    }
+    SceneView sc;
+    sc.sph = kLds ? s_sph : a.sph;
+    sc.mats = a.mats;
+    sc.lights = a.lights;
+    sc.count = a.count;
+    sc.nlights = a.nlights;
+
+    // 16x16 tile = 4 waves of 8x8 pixels
+    const int wave = tid >> 6, lane = tid & 63;
+    const int lx = blockIdx.x * kTileX + (wave & 1) * 8 + (lane & 7);
+    const int ly = blockIdx.y * kTileY + (wave >> 1) * 8 + (lane >> 3);
+    int rays = 0;
+    if (lx < a.xc && ly < a.rows) {
+        const int x = a.x0 + lx;
+        const int y = a.y0 + (ly / a.rb) * a.rb * a.rp + a.rph * a.rb + ly % a.rb;
+        const float invWidth = 1.0f / (float)a.width;     // parallel.cpp:260
+        const float invHeight = 1.0f / (float)a.height;   // parallel.cpp:261
+        float4* px = a.out + (size_t)ly * a.xc + lx;
+        float4 acc = *px;
+        for (int f = a.frame0; f < a.frame0 + a.frames; ++f) {
+            uint32_t rng = PixelSeed((uint32_t)x, (uint32_t)y, (uint32_t)f);
+            const float lerpFac = (float)f / (float)(f + 1);                  // :262
+            float u = ((float)x + RandomFloat01(rng)) * invWidth;              // :272
+            float v = ((float)y + RandomFloat01(rng)) * invHeight;             // :273
+            Ray r = GetRay(a.cam, u, v, rng);
+            F3 col = Trace<MAXD>(r, a.maxDepth, rays, rng, sc);
+            F3 prev = f3(acc.x, acc.y, acc.z);
+            col = prev * lerpFac + col * (1.0f - lerpFac);                     // :282
+            acc.x = col.x;
+            acc.y = col.y;
+            acc.z = col.z;
+        }
+        *px = acc;
+    }
+    unsigned long long total = wave_sum((unsigned long long)rays);
+    if (lane == 0 && total) atomicAdd(a.rays, total);
+}
+
+// Frame assembly: shard g's local row ly -> global row (as lrt_render_desc's map).
+__global__ void unshard_kernel(const float4* __restrict__ src, float4* __restrict__ dst, int width, int height,
+                               int rb, int period, int maxRows) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    if (x >= width || y >= height) return;
+    const int blk = y / rb;
+    const int g = blk % period;
+    const int ly = (blk / period) * rb + y % rb;
+    dst[(size_t)y * width + x] = src[((size_t)g * maxRows + ly) * width + x];
+}
+
+// LinearToSRGB + pack (main.cpp:109-141): b | g << 8 | r << 16 per pixel.
+LRT_DEV uint32_t linear_to_srgb(float x) {   // main.cpp:109-115
+    x = (x < 0.0f) ? 0.0f : x;                                   // std::max(x, 0.0f)
+    x = 1.055f * libm::powf(x, 0.416666667f) - 0.055f;
+    x = (x < 0.0f) ? 0.0f : x;                                   // std::max(..., 0.0f)
+    uint32_t u = (uint32_t)(x * 255.9f);
+    return u < 255u ? u : 255u;                                  // std::min(u, 255u)
+}
+__global__ void present_kernel(const float4* __restrict__ src, uint32_t* __restrict__ dst, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float4 c = src[i];
+    dst[i] = linear_to_srgb(c.z) | (linear_to_srgb(c.y) << 8) | (linear_to_srgb(c.x) << 16);
+}
+
+LRT_HD float libm_eval(int kind, float x) {
+    return kind == 0 ? libm::sinf(x) : kind == 1 ? libm::cosf(x) : kind == 2 ? libm::powf5(x)
+                                                                            : libm::powf(x, 0.416666667f);
+}
+
+__global__ void libm_kernel(int kind, const float* __restrict__ in, float* __restrict__ out, long long n) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float x = in[i];
+    out[i] = libm_eval(kind, x);
+}
+
+// ---------------------------------------------------------------------------------
+// host side
+struct Context {
+    bool ready = false;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int count = 0, nlights = 0;
+    float4* d_sph = nullptr;
+    float4* d_mats = nullptr;
+    int* d_lights = nullptr;
+    std::vector<lrt_sphere> spheres;
+    std::vector<lrt_material> mats;
+    float* d_frame = nullptr;   // lrt_draw_test / lrt_render_host staging
+    size_t frame_bytes = 0;
+    unsigned long long* d_rays = nullptr;
+};
+
+Context g_ctx;
+std::mutex g_mu;
+thread_local std::string t_err;
+
+int fail(int code, const std::string& msg) {
+    t_err = msg;
+    return code;
+}
+int hip_fail(hipError_t e, const char* what) {
+    return fail(LRT_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+#define LRT_HIP(call)                                            \
+    do {                                                         \
+        hipError_t _e = (call);                                  \
+        if (_e != hipSuccess) return hip_fail(_e, #call);        \
+    } while (0)
+
+// parallel.cpp:15-51
+const lrt_sphere kDefaultSpheres[9] = {
+    {{0, -100.5f, -1}, 100.0f}, {{2, 1, -1}, 0.5f},  {{0, 0, -1}, 0.5f},
+    {{-2, 0, -1}, 0.5f},        {{2, 0, 1}, 0.5f},   {{0, 0, 1}, 0.5f},
+    {{-2, 0, 1}, 0.5f},         {{0.5f, 1, 0.5f}, 0.5f}, {{-1.5f, 1.5f, 0.f}, 0.3f},
+};
+const lrt_material kDefaultMats[9] = {
+    {LRT_LAMBERT, {0.8f, 0.8f, 0.8f}, {0, 0, 0}, 0, 0},
+    {LRT_LAMBERT, {0.8f, 0.4f, 0.4f}, {0, 0, 0}, 0, 0},
+    {LRT_LAMBERT, {0.4f, 0.8f, 0.4f}, {0, 0, 0}, 0, 0},
+    {LRT_METAL, {0.4f, 0.4f, 0.8f}, {0, 0, 0}, 0, 0},
+    {LRT_METAL, {0.4f, 0.8f, 0.4f}, {0, 0, 0}, 0, 0},
+    {LRT_METAL, {0.4f, 0.8f, 0.4f}, {0, 0, 0}, 0.2f, 0},
+    {LRT_METAL, {0.4f, 0.8f, 0.4f}, {0, 0, 0}, 0.6f, 0},
+    {LRT_DIELECTRIC, {0.4f, 0.4f, 0.4f}, {0, 0, 0}, 0, 1.5f},
+    {LRT_LAMBERT, {0.8f, 0.6f, 0.2f}, {30, 25, 15}, 0, 0},
+};
+
+void free_scene(Context& c) {
+    if (c.d_sph) (void)hipFree(c.d_sph);
+    if (c.d_mats) (void)hipFree(c.d_mats);
+    if (c.d_lights) (void)hipFree(c.d_lights);
+    c.d_sph = nullptr;
+    c.d_mats = nullptr;
+    c.d_lights = nullptr;
+}
+
+int upload_scene(Context& c, const lrt_sphere* s, const lrt_material* m, int n) {
+    if (!s || !m || n < 1 || n > LRT_MAX_SPHERES) return fail(LRT_E_INVALID, "scene: need 1..LRT_MAX_SPHERES spheres");
+    std::vector<float4> sph(n), mats(3 * (size_t)n);
+    std::vector<int> lights;
+    for (int i = 0; i < n; ++i) {
+        if (m[i].type < 0 || m[i].type > 2) return fail(LRT_E_INVALID, "scene: material type must be 0..2");
+        const float r = s[i].radius;
+        sph[i] = make_float4(s[i].center.x, s[i].center.y, s[i].center.z, r * r);
+        const bool diel = m[i].type == LRT_DIELECTRIC;
+        int type = m[i].type;
+        float typef;
+        memcpy(&typef, &type, 4);
+        mats[3 * i + 0] = make_float4(m[i].albedo.x, m[i].albedo.y, m[i].albedo.z, typef);
+        mats[3 * i + 1] = make_float4(m[i].emissive.x, m[i].emissive.y, m[i].emissive.z, m[i].roughness);
+        mats[3 * i + 2] = diel ? make_float4(1.0f, 1.0f, 1.0f, m[i].ri)
+                               : make_float4(m[i].albedo.x, m[i].albedo.y, m[i].albedo.z, m[i].ri);
+        // parallel.cpp:96: skip only if every channel <= 0
+        if (!(m[i].emissive.x <= 0 && m[i].emissive.y <= 0 && m[i].emissive.z <= 0)) lights.push_back(i);
+    }
+    free_scene(c);
+    LRT_HIP(hipMalloc(&c.d_sph, sizeof(float4) * n));
+    LRT_HIP(hipMalloc(&c.d_mats, sizeof(float4) * 3 * n));
+    LRT_HIP(hipMalloc(&c.d_lights, sizeof(int) * (lights.empty() ? 1 : lights.size())));
+    LRT_HIP(hipMemcpy(c.d_sph, sph.data(), sizeof(float4) * n, hipMemcpyHostToDevice));
+    LRT_HIP(hipMemcpy(c.d_mats, mats.data(), sizeof(float4) * 3 * n, hipMemcpyHostToDevice));
+    if (!lights.empty())
+        LRT_HIP(hipMemcpy(c.d_lights, lights.data(), sizeof(int) * lights.size(), hipMemcpyHostToDevice));
+    c.count = n;
+    c.nlights = (int)lights.size();
+    c.spheres.assign(s, s + n);
+    c.mats.assign(m, m + n);
+    return LRT_OK;
+}
+
+lrt_float3 L3(float x, float y, float z) {
+    lrt_float3 r = {x, y, z};
+    return r;
+}
+// Host float3 helpers for the camera constructor (maths.h:63-97).
+lrt_float3 h_sub(lrt_float3 a, lrt_float3 b) { return L3(a.x - b.x, a.y - b.y, a.z - b.z); }
+lrt_float3 h_smul(float a, lrt_float3 b) { return L3(a * b.x, a * b.y, a * b.z); }
+lrt_float3 h_cross(lrt_float3 a, lrt_float3 b) {
+    return L3(a.y * b.z - a.z * b.y, -(a.x * b.z - a.z * b.x), a.x * b.y - a.y * b.x);
+}
+lrt_float3 h_normalize(lrt_float3 v) {
+    float k = 1.0f / sqrtf(v.x * v.x + v.y * v.y + v.z * v.z);
+    return L3(v.x * k, v.y * k, v.z * k);
+}
+
+int validate(const lrt_render_desc* d) {
+    if (!d) return fail(LRT_E_INVALID, "desc is NULL");
+    if (d->width < 1 || d->height < 1) return fail(LRT_E_INVALID, "width/height must be >= 1");
+    if (d->x0 < 0 || d->x_count < 0 || (long long)d->x0 + d->x_count > d->width)
+        return fail(LRT_E_INVALID, "column window outside the image");
+    if (d->row_block < 1 || d->row_period < 1 || d->row_phase < 0 || d->row_phase >= d->row_period)
+        return fail(LRT_E_INVALID, "row_block/row_period/row_phase invalid");
+    if (d->y0 < 0 || d->row_count < 0) return fail(LRT_E_INVALID, "y0/row_count must be >= 0");
+    if (d->row_count > 0) {
+        long long ly = d->row_count - 1;
+        long long y = d->y0 + (ly / d->row_block) * (long long)d->row_block * d->row_period +
+                      (long long)d->row_phase * d->row_block + ly % d->row_block;
+        if (y >= d->height) return fail(LRT_E_INVALID, "local rows map outside the image");
+    }
+    if (d->frame0 < 0 || d->frames < 0) return fail(LRT_E_INVALID, "frame0/frames must be >= 0");
+    if ((long long)d->frame0 + d->frames > 0x7fffffffLL) return fail(LRT_E_INVALID, "frame range overflows int");
+    if (d->max_depth < 0 || d->max_depth > kMaxDepthSupported)
+        return fail(LRT_E_INVALID, "max_depth must be in 0..64");
+    return LRT_OK;
+}
+
+template <int MAXD>
+hipError_t launch_depth(const KernelArgs& a, bool lds, dim3 grid, hipStream_t s) {
+    if (lds) {
+        trace_kernel<MAXD, true><<<grid, kBlock, sizeof(float4) * a.count, s>>>(a);
+    } else {
+        trace_kernel<MAXD, false><<<grid, kBlock, 0, s>>>(a);
+    }
+    return hipGetLastError();
+}
+
+int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_rays, hipStream_t s) {
+    int rc = validate(d);
+    if (rc) return rc;
+    if (!g_ctx.ready) return fail(LRT_E_STATE, "lrt_initialize() has not been called");
+    if (!d_buf || !d_rays) return fail(LRT_E_INVALID, "device buffer / ray counter is NULL");
+    if (d->x_count == 0 || d->row_count == 0 || d->frames == 0) return LRT_OK;
+    KernelArgs a;
+    const lrt_camera& c = d->camera;
+    a.cam.origin = f3(c.origin.x, c.origin.y, c.origin.z);
+    a.cam.a = f3(c.a.x, c.a.y, c.a.z);
+    a.cam.u = f3(c.u.x, c.u.y, c.u.z);
+    a.cam.r = f3(c.r.x, c.r.y, c.r.z);
+    a.cam.llc = f3(c.lowerLeftCorner.x, c.lowerLeftCorner.y, c.lowerLeftCorner.z);
+    a.cam.horiz = f3(c.horizontalVec.x, c.horizontalVec.y, c.horizontalVec.z);
+    a.cam.vert = f3(c.verticalVec.x, c.verticalVec.y, c.verticalVec.z);
+    a.cam.lensRadius = c.lensRadius;
+    a.sph = g_ctx.d_sph;
+    a.mats = g_ctx.d_mats;
+    a.lights = g_ctx.d_lights;
+    a.count = g_ctx.count;
+    a.nlights = g_ctx.nlights;
+    a.width = d->width;
+    a.height = d->height;
+    a.x0 = d->x0;
+    a.xc = d->x_count;
+    a.y0 = d->y0;
+    a.rows = d->row_count;
+    a.rb = d->row_block;
+    a.rp = d->row_period;
+    a.rph = d->row_phase;
+    a.frame0 = d->frame0;
+    a.frames = d->frames;
+    a.maxDepth = d->max_depth;
+    a.out = reinterpret_cast<float4*>(d_buf);
+    a.rays = d_rays;
+    const bool lds = !(d->flags & LRT_F_SCENE_GLOBAL) && a.count <= kLdsSphereLimit;
+    dim3 grid((d->x_count + kTileX - 1) / kTileX, (d->row_count + kTileY - 1) / kTileY);
+    hipError_t e;
+    if (d->max_depth <= 8)
+        e = launch_depth<8>(a, lds, grid, s);
+    else if (d->max_depth <= 20)
+        e = launch_depth<20>(a, lds, grid, s);
+    else
+        e = launch_depth<64>(a, lds, grid, s);
+    if (e != hipSuccess) return hip_fail(e, "trace_kernel launch");
+    return LRT_OK;
+}
+
+int ensure_frame(size_t bytes) {
+    if (g_ctx.frame_bytes >= bytes) return LRT_OK;
+    if (g_ctx.d_frame) (void)hipFree(g_ctx.d_frame);
+    g_ctx.d_frame = nullptr;
+    g_ctx.frame_bytes = 0;
+    if (hipMalloc(&g_ctx.d_frame, bytes) != hipSuccess) return fail(LRT_E_NOMEM, "hipMalloc(frame) failed");
+    g_ctx.frame_bytes = bytes;
+    return LRT_OK;
+}
+
+int render_host(const lrt_render_desc* d, float* buf, long long* out_rays) {
+    int rc = validate(d);
+    if (rc) return rc;
+    if (!g_ctx.ready) return fail(LRT_E_STATE, "lrt_initialize() has not been called");
+    if (!buf) return fail(LRT_E_INVALID, "backbuffer is NULL");
+    const size_t bytes = (size_t)d->x_count * d->row_count * 4 * sizeof(float);
+    if (bytes == 0 || d->frames == 0) {
+        if (out_rays) *out_rays = 0;
+        return LRT_OK;
+    }
+    if ((rc = ensure_frame(bytes))) return rc;
+    hipStream_t s = g_ctx.stream;
+    LRT_HIP(hipMemcpyAsync(g_ctx.d_frame, buf, bytes, hipMemcpyHostToDevice, s));
+    LRT_HIP(hipMemsetAsync(g_ctx.d_rays, 0, sizeof(unsigned long long), s));
+    if ((rc = render_device(d, g_ctx.d_frame, g_ctx.d_rays, s))) return rc;
+    unsigned long long rays = 0;
+    LRT_HIP(hipMemcpyAsync(buf, g_ctx.d_frame, bytes, hipMemcpyDeviceToHost, s));
+    LRT_HIP(hipMemcpyAsync(&rays, g_ctx.d_rays, sizeof(rays), hipMemcpyDeviceToHost, s));
+    LRT_HIP(hipStreamSynchronize(s));
+    if (out_rays) *out_rays = (long long)rays;
+    return LRT_OK;
+}
+
+int camera_make(lrt_float3 lookFrom, lrt_float3 lookAt, lrt_float3 vup, float vfov, float aspect, float aperture,
+                float focusDist, lrt_camera* out) {   // maths.h:183-202
+    if (!out) return fail(LRT_E_INVALID, "camera out is NULL");
+    lrt_camera c;
+    c.lensRadius = aperture / 2.0f;
+    c.origin = lookFrom;
+    c.a = h_normalize(h_sub(lookFrom, lookAt));
+    c.r = h_normalize(h_cross(vup, c.a));
+    c.u = h_normalize(h_cross(c.a, c.r));
+    float theta = vfov * kPI / 180.0f;
+    float halfHeightTan = tanf(theta / 2.0f);
+    float halfWidthTan = aspect * halfHeightTan;
+    c.lowerLeftCorner = h_sub(h_sub(h_sub(c.origin, h_smul(halfWidthTan * focusDist, c.r)),
+                                    h_smul(halfHeightTan * focusDist, c.u)),
+                              h_smul(focusDist, c.a));
+    c.horizontalVec = h_smul(2.0f * halfWidthTan * focusDist, c.r);
+    c.verticalVec = h_smul(2.0f * halfHeightTan * focusDist, c.u);
+    *out = c;
+    return LRT_OK;
+}
+
+int camera_default(int w, int h, lrt_camera* out) {   // parallel.cpp:299-307
+    if (w < 1 || h < 1) return fail(LRT_E_INVALID, "width/height must be >= 1");
+    return camera_make(L3(0, 2, 3), L3(0, 0, 0), L3(0, 1, 0), 60.0f, (float)w / (float)h, 0.1f, 3.0f, out);
+}
+
+}  // namespace lrt
+
+using namespace lrt;
+
+extern "C" {
+
+const char* lrt_last_error(void) { return t_err.c_str(); }
+const char* lrt_version(void) { return LRT_VERSION_STRING; }
+
+int lrt_initialize(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_ctx.ready) return LRT_OK;
+    int dev = 0;
+    LRT_HIP(hipGetDevice(&dev));
+    g_ctx.device = dev;
+    LRT_HIP(hipStreamCreateWithFlags(&g_ctx.stream, hipStreamNonBlocking));
+    LRT_HIP(hipMalloc(&g_ctx.d_rays, sizeof(unsigned long long)));
+    int rc = upload_scene(g_ctx, kDefaultSpheres, kDefaultMats, 9);
+    if (rc) return rc;
+    g_ctx.ready = true;
+    return LRT_OK;
+}
+
+int lrt_shutdown(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_ctx.ready) return LRT_OK;
+    (void)hipDeviceSynchronize();
+    free_scene(g_ctx);
+    if (g_ctx.d_frame) (void)hipFree(g_ctx.d_frame);
+    if (g_ctx.d_rays) (void)hipFree(g_ctx.d_rays);
+    if (g_ctx.stream) (void)hipStreamDestroy(g_ctx.stream);
+    g_ctx = Context();
+    return LRT_OK;
+}
+
+int lrt_draw_test(float time, int frameCount, int screenWidth, int screenHeight, float* backbuffer,
+                  int* outRayCount) {
+    (void)time;   // unused by the reference too (JobData::time, parallel.cpp:244)
+    std::lock_guard<std::mutex> lk(g_mu);
+    lrt_render_desc d;
+    memset(&d, 0, sizeof(d));
+    int rc = camera_default(screenWidth, screenHeight, &d.camera);
+    if (rc) return rc;
+    d.width = screenWidth;
+    d.height = screenHeight;
+    d.x0 = 0;
+    d.x_count = screenWidth;
+    d.y0 = 0;
+    d.row_count = screenHeight;
+    d.row_block = screenHeight;
+    d.row_period = 1;
+    d.row_phase = 0;
+    d.frame0 = frameCount;
+    d.frames = 1;
+    d.max_depth = LRT_REFERENCE_MAX_DEPTH;
+    long long rays = 0;
+    rc = render_host(&d, backbuffer, &rays);
+    if (rc) return rc;
+    if (outRayCount) *outRayCount = (int)rays;
+    return LRT_OK;
+}
+
+int lrt_camera_make(lrt_float3 lookFrom, lrt_float3 lookAt, lrt_float3 vup, float vfov, float aspect,
+                    float aperture, float focusDist, lrt_camera* out) {
+    return camera_make(lookFrom, lookAt, vup, vfov, aspect, aperture, focusDist, out);
+}
+
+int lrt_camera_default(int width, int height, lrt_camera* out) { return camera_default(width, height, out); }
+
+int lrt_set_scene(const lrt_sphere* spheres, const lrt_material* materials, int count) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_ctx.ready) return fail(LRT_E_STATE, "lrt_initialize() has not been called");
+    LRT_HIP(hipStreamSynchronize(g_ctx.stream));
+    LRT_HIP(hipDeviceSynchronize());
+    return upload_scene(g_ctx, spheres, materials, count);
+}
+
+int lrt_default_scene(lrt_sphere* spheres, lrt_material* materials, int capacity, int* count) {
+    if (count) *count = 9;
+    if (capacity < 9 || !spheres || !materials) return fail(LRT_E_INVALID, "need capacity >= 9");
+    memcpy(spheres, kDefaultSpheres, sizeof(kDefaultSpheres));
+    memcpy(materials, kDefaultMats, sizeof(kDefaultMats));
+    return LRT_OK;
+}
+
+int lrt_render_device(const lrt_render_desc* desc, float* d_backbuffer, unsigned long long* d_rays, void* stream) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    return render_device(desc, d_backbuffer, d_rays, stream ? (hipStream_t)stream : g_ctx.stream);
+}
+
+int lrt_render_host(const lrt_render_desc* desc, float* backbuffer, long long* out_rays) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    return render_host(desc, backbuffer, out_rays);
+}
+
+int lrt_shard_rows(int height, int row_block, int period, int phase) {
+    if (height < 0 || row_block < 1 || period < 1 || phase < 0 || phase >= period)
+        return fail(LRT_E_INVALID, "invalid shard geometry");
+    int blocks = (height + row_block - 1) / row_block;
+    int rows = 0;
+    for (int b = phase; b < blocks; b += period) {
+        int top = (b + 1) * row_block;
+        rows += (top > height ? height : top) - b * row_block;
+    }
+    return rows;
+}
+
+int lrt_unshard_rows(const float* d_src, float* d_dst, int width, int height, int row_block, int period,
+                     void* stream) {
+    if (!d_src || !d_dst || width < 1 || height < 1 || row_block < 1 || period < 1)
+        return fail(LRT_E_INVALID, "invalid unshard arguments");
+    int maxRows = lrt_shard_rows(height, row_block, period, 0);
+    hipStream_t s = stream ? (hipStream_t)stream : g_ctx.stream;
+    dim3 grid((width + 255) / 256, height);
+    unshard_kernel<<<grid, 256, 0, s>>>(reinterpret_cast<const float4*>(d_src), reinterpret_cast<float4*>(d_dst),
+                                        width, height, row_block, period, maxRows);
+    LRT_HIP(hipGetLastError());
+    return LRT_OK;
+}
+
+int lrt_present_bgra8(const float* d_rgba, uint32_t* d_bgra, int width, int height, void* stream) {
+    if (!d_rgba || !d_bgra || width < 1 || height < 1) return fail(LRT_E_INVALID, "invalid present arguments");
+    int n = width * height;
+    hipStream_t s = stream ? (hipStream_t)stream : g_ctx.stream;
+    present_kernel<<<(n + 255) / 256, 256, 0, s>>>(reinterpret_cast<const float4*>(d_rgba), d_bgra, n);
+    LRT_HIP(hipGetLastError());
+    return LRT_OK;
+}
+
+int lrt_libm_eval_host(int kind, const float* in, float* out, long long n) {
+    if (kind < 0 || kind > 3 || !in || !out || n < 0) return fail(LRT_E_INVALID, "invalid libm eval arguments");
+    for (long long i = 0; i < n; ++i)
+        out[i] = libm_eval(kind, in[i]);
+    return LRT_OK;
+}
+
+int lrt_libm_eval_device(int kind, const float* d_in, float* d_out, long long n) {
+    if (kind < 0 || kind > 3 || !d_in || !d_out || n < 0) return fail(LRT_E_INVALID, "invalid libm eval arguments");
+    if (n == 0) return LRT_OK;
+    libm_kernel<<<(unsigned)((n + 255) / 256), 256, 0, nullptr>>>(kind, d_in, d_out, n);
+    LRT_HIP(hipGetLastError());
+    LRT_HIP(hipDeviceSynchronize());
+    return LRT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,306 @@
+// Device restatement of the reference hot path (src/cpu/maths.{h,cpp}, parallel.cpp),
+// written for one work-item per pixel on gfx950.
+//
+// Parity rules are kept literally: left-to-right RNG draw order,
+// XorShift32 13/17/15, rejection tests, double normalisation, member vs free
+// normalize, the reference's association order in every expression, glibc-exact
+// transcendentals (lrt_libm.h), IEEE sqrt/div, and the build uses
+// -ffp-contract=off so no a*b+c is fused. The recursive Trace() is flattened into a
+// loop that pushes (matE + lightE, material) per scatter event and then folds the
+// stack from the leaf outwards, which evaluates exactly the reference's
+// `matE + lightE + attenuation * Trace(...)` (parallel.cpp:214) in the same order.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lrt_libm.h"
+
+namespace lrt {
+
+#define LRT_DEV __host__ __device__ __forceinline__
+
+constexpr float kPI = 3.1415926f;     // maths.h:5
+constexpr float kMinT = 0.001f;       // parallel.cpp:9
+constexpr float kMaxT = 1.0e7f;       // parallel.cpp:10
+
+struct float3_ { float x, y, z; };    // maths.h:10-61 (own type: no vendor operators)
+using F3 = float3_;
+
+LRT_DEV F3 f3(float x, float y, float z) { F3 r; r.x = x; r.y = y; r.z = z; return r; }
+LRT_DEV F3 operator+(F3 a, F3 b) { return f3(a.x + b.x, a.y + b.y, a.z + b.z); }   // maths.h:63
+LRT_DEV F3 operator-(F3 a, F3 b) { return f3(a.x - b.x, a.y - b.y, a.z - b.z); }   // maths.h:67
+LRT_DEV F3 operator*(F3 a, F3 b) { return f3(a.x * b.x, a.y * b.y, a.z * b.z); }   // maths.h:71
+LRT_DEV F3 operator*(F3 a, float b) { return f3(a.x * b, a.y * b, a.z * b); }      // maths.h:75
+LRT_DEV F3 operator*(float a, F3 b) { return f3(a * b.x, a * b.y, a * b.z); }      // maths.h:79
+LRT_DEV F3 operator-(F3 a) { return f3(-a.x, -a.y, -a.z); }                        // maths.h:27
+LRT_DEV float dot(F3 a, F3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }        // maths.h:83
+LRT_DEV F3 cross(F3 a, F3 b) {                                                      // maths.h:87-92
+    return f3(a.y * b.z - a.z * b.y, -(a.x * b.z - a.z * b.x), a.x * b.y - a.y * b.x);
+}
+LRT_DEV float length(F3 v) { return __builtin_sqrtf(v.x * v.x + v.y * v.y + v.z * v.z); } // maths.h:15
+LRT_DEV F3 normalize(F3 v) { float k = 1.0f / length(v); return f3(v.x * k, v.y * k, v.z * k); } // maths.h:93
+LRT_DEV F3 normalize_member(F3 v) { float l = length(v); return f3(v.x / l, v.y / l, v.z / l); } // maths.h:19
+LRT_DEV F3 reflect(F3 v, F3 n) { return v + 2.0f * (-dot(v, n) * n); }             // maths.h:100-103
+LRT_DEV bool refract(F3 v, F3 n, float nint, F3& out) {                             // maths.h:106-118
+    float dt = dot(v, n);
+    float discr = 1.0f - nint * nint * (1.0f - dt * dt);
+    if (discr > 0) {
+        out = nint * (v - n * dt) - n * __builtin_sqrtf(discr);
+        return true;
+    }
+    return false;
+}
+LRT_DEV float schlick(float cosine, float ri) {                                     // maths.h:122-127
+    float r0 = (1.0f - ri) / (1.0f + ri);
+    r0 = r0 * r0;
+    return r0 + (1.0f - r0) * libm::powf5(1.0f - cosine);
+}
+
+struct Ray {                                                                        // maths.h:130-145
+    F3 orig, dir;
+};
+LRT_DEV Ray make_ray(F3 o, F3 d) { Ray r; r.orig = o; r.dir = normalize(d); return r; }
+LRT_DEV F3 point_at(const Ray& r, float t) { return r.orig + r.dir * t; }
+
+struct Hit { F3 pos, normal; float t; };                                            // maths.h:148-153
+
+// ---- RNG: maths.cpp:7-49 with the state in a register (one stream per pixel-sample)
+LRT_DEV uint32_t XorShift32(uint32_t& s) {
+    uint32_t x = s;
+    x ^= x << 13;
+    x ^= x >> 17;
+    x ^= x << 15;
+    s = x;
+    return x;
+}
+LRT_DEV float RandomFloat01(uint32_t& s) { return (float)(XorShift32(s) & 0xFFFFFF) * (1.0f / 16777216.0f); }
+LRT_DEV F3 RandomInUnitDisk(uint32_t& s) {
+    F3 p;
+    do {
+        float a = RandomFloat01(s);
+        float b = RandomFloat01(s);
+        p = 2.0f * f3(a, b, 0.0f) - f3(1.0f, 1.0f, 0.0f);
+    } while (dot(p, p) >= 1.0f);
+    return p;
+}
+LRT_DEV F3 RandomUnitVector(uint32_t& s) {
+    float z = RandomFloat01(s) * 2.0f - 1.0f;
+    float a = RandomFloat01(s) * 2.0f * kPI;
+    float r = __builtin_sqrtf(1.0f - z * z);
+    float x = r * libm::cosf(a);
+    float y = r * libm::sinf(a);
+    return f3(x, y, z);
+}
+LRT_DEV F3 RandomInUnitSphere(uint32_t& s) {
+    F3 p;
+    do {
+        float a = RandomFloat01(s);
+        float b = RandomFloat01(s);
+        float c = RandomFloat01(s);
+        p = 2.0f * f3(a, b, c) - f3(1.0f, 1.0f, 1.0f);
+    } while (length(p) >= 1.0f);
+    return p;
+}
+
+// ---- scene as the kernel sees it -------------------------------------------------
+// Sphere: float4(center.xyz, radius*radius). The reference only ever uses the radius
+// squared (maths.cpp:59, parallel.cpp:109), so r*r is folded once on the host.
+// Material: three float4 rows: (albedo.xyz, type), (emissive.xyz, roughness),
+// (attenuation.xyz, ri) where attenuation = albedo (Lambert, Metal) or 1 (Dielectric,
+// parallel.cpp:90,144,192).
+struct Material {
+    F3 albedo;
+    int type;
+    F3 emissive;
+    float roughness;
+    F3 att;
+    float ri;
+};
+LRT_DEV Material load_material(const float4* __restrict__ mats, int id) {
+    float4 a = mats[3 * id + 0];
+    float4 e = mats[3 * id + 1];
+    float4 b = mats[3 * id + 2];
+    Material m;
+    m.albedo = f3(a.x, a.y, a.z);
+    m.type = __float_as_int(a.w);
+    m.emissive = f3(e.x, e.y, e.z);
+    m.roughness = e.w;
+    m.att = f3(b.x, b.y, b.z);
+    m.ri = b.w;
+    return m;
+}
+
+struct SceneView {
+    const float4* sph;                 // LDS or global
+    const float4* __restrict__ mats;   // global (per-lane gather, L1/L2 resident)
+    const int* __restrict__ lights;    // emissive sphere ids in index order
+    int count;
+    int nlights;
+};
+
+// HitWorld + HitSphere (parallel.cpp:54-73, maths.cpp:51-94). The per-sphere test
+// is the reference's; hit position and normal are computed once for the winner
+// (they are pure functions of (ray, t, sphere), so this is bit-identical to the
+// reference overwriting them on every closer hit).
+LRT_DEV bool HitWorld(const Ray& r, float tMin, float tMax, const SceneView& sc, Hit& outHit, int& outID) {
+    float closestT = tMax;
+    int id = -1;
+    for (int i = 0; i < sc.count; ++i) {
+        float4 s = sc.sph[i];
+        F3 rs = f3(s.x, s.y, s.z) - r.orig;
+        float rsProj = dot(rs, r.dir);
+        float ifHit = dot(rs, rs) - rsProj * rsProj - s.w;
+        if (ifHit < 0.0f) {
+            float halfCut = __builtin_sqrtf(-ifHit);
+            float t = rsProj - halfCut;
+            if (t > tMin && t < closestT) {
+                closestT = t;
+                id = i;
+            } else {
+                t = rsProj + halfCut;
+                if (t > tMin && t < closestT) {
+                    closestT = t;
+                    id = i;
+                }
+            }
+        }
+    }
+    if (id < 0) return false;
+    float4 s = sc.sph[id];
+    outHit.pos = point_at(r, closestT);
+    outHit.normal = normalize(outHit.pos - f3(s.x, s.y, s.z));
+    outHit.t = closestT;
+    outID = id;
+    return true;
+}
+
+// Scatter (parallel.cpp:78-196). The reference's `&mat == &smat` self test is the
+// comparison of table indices (matId). lightE accumulates in the same order.
+LRT_DEV bool Scatter(const Material& mat, int matId, const Ray& r_in, const Hit& rec, F3& attenuation,
+                     Ray& scattered, F3& outLightE, int& inoutRayCount, uint32_t& rng, const SceneView& sc) {
+    outLightE = f3(0.0f, 0.0f, 0.0f);
+    if (mat.type == 0) {  // Lambert :81-136
+        F3 target = rec.pos + rec.normal + RandomUnitVector(rng);
+        scattered = make_ray(rec.pos, normalize(target - rec.pos));
+        attenuation = mat.albedo;
+        for (int k = 0; k < sc.nlights; ++k) {
+            int i = sc.lights[k];
+            if (i == matId) continue;  // :98
+            float4 s = sc.sph[i];
+            F3 c = f3(s.x, s.y, s.z);
+            F3 sw = normalize(c - rec.pos);
+            F3 su = normalize(cross(__builtin_fabsf(sw.x) > 0.01f ? f3(0.0f, 1.0f, 0.0f) : f3(1.0f, 0.0f, 0.0f), sw));
+            F3 sv = cross(sw, su);
+            float len = length(rec.pos - c);
+            float cosAMax = __builtin_sqrtf(1.0f - s.w / (len * len));                    // :109
+            float eps1 = RandomFloat01(rng);
+            float eps2 = RandomFloat01(rng);
+            float cosA = 1.0f - eps1 + eps1 * cosAMax;
+            float sinA = __builtin_sqrtf(1.0f - cosA * cosA);
+            float phi = 2.0f * kPI * eps2;
+            F3 l = su * libm::cosf(phi) * sinA + sv * libm::sinf(phi) * sinA + sw * cosA;   // :116
+            l = normalize_member(l);                                                      // :117
+            Hit lightHit;
+            int hitID = -1;
+            ++inoutRayCount;                                                              // :122
+            if (HitWorld(make_ray(rec.pos, l), kMinT, kMaxT, sc, lightHit, hitID) && hitID == i) {
+                float omega = 2.0f * kPI * (1.0f - cosAMax);
+                F3 rdir = r_in.dir;
+                F3 nl = dot(rec.normal, rdir) < 0.0f ? rec.normal : -rec.normal;
+                float d = dot(l, nl);
+                float mx = (0.0f < d) ? d : 0.0f;   // std::max(0.0f, d)
+                const float4 e = sc.mats[3 * i + 1];
+                outLightE = outLightE + (mat.albedo * f3(e.x, e.y, e.z)) * (mx * omega / kPI);
+            }
+        }
+        return true;
+    } else if (mat.type == 1) {  // Metal :137-148
+        F3 refl = reflect(r_in.dir, rec.normal);
+        scattered = make_ray(rec.pos, normalize(refl + mat.roughness * RandomInUnitSphere(rng)));
+        attenuation = mat.albedo;
+        return dot(scattered.dir, rec.normal) > 0.0f;
+    } else if (mat.type == 2) {  // Dielectric :149-193
+        F3 outwardN;
+        F3 rdir = r_in.dir;
+        F3 refl = reflect(rdir, rec.normal);
+        float nint;
+        F3 refr = f3(0.0f, 0.0f, 0.0f);
+        float reflProb;
+        float cosine;
+        if (dot(rdir, rec.normal) > 0.0f) {
+            outwardN = -rec.normal;
+            nint = mat.ri;
+            cosine = dot(rdir, rec.normal);
+        } else {
+            outwardN = rec.normal;
+            nint = 1.0f / mat.ri;
+            cosine = -dot(rdir, rec.normal);
+        }
+        if (refract(rdir, outwardN, nint, refr))
+            reflProb = schlick(cosine, mat.ri);
+        else
+            reflProb = 1.0f;
+        if (RandomFloat01(rng) < reflProb)
+            scattered = make_ray(rec.pos, normalize(refl));
+        else
+            scattered = make_ray(rec.pos, normalize(refr));
+        attenuation = f3(1.0f, 1.0f, 1.0f);
+    }
+    return true;
+}
+
+// Trace (parallel.cpp:200-227) as a loop. Scatter events are pushed on a per-lane
+// stack of (matE + lightE, material id); the fold T = E + att * T from the leaf
+// outwards reproduces the recursion's rounding exactly. maxDepth scatter events at
+// most (the reference's depth < kMaxDepth test); MAXD >= maxDepth.
+template <int MAXD>
+LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const SceneView& sc) {
+    float4 stack[MAXD > 0 ? MAXD : 1];
+    int depth = 0;
+    F3 leaf;
+    for (;;) {
+        Hit rec;
+        int id = 0;
+        ++inoutRayCount;
+        if (!HitWorld(r, kMinT, kMaxT, sc, rec, id)) {
+            float t = 0.5f * (r.dir.y + 1.0f);
+            leaf = ((1.0f - t) * f3(1.0f, 1.0f, 1.0f) + t * f3(0.5f, 0.7f, 1.0f)) * 0.3f;
+            break;
+        }
+        Material mat = load_material(sc.mats, id);
+        F3 matE = mat.emissive;
+        Ray scattered;
+        F3 attenuation, lightE;
+        if (depth < maxDepth &&
+            Scatter(mat, id, r, rec, attenuation, scattered, lightE, inoutRayCount, rng, sc)) {
+            F3 e = matE + lightE;
+            stack[depth] = make_float4(e.x, e.y, e.z, __int_as_float(id));
+            ++depth;
+            r = scattered;
+            continue;
+        }
+        leaf = matE;
+        break;
+    }
+    F3 T = leaf;
+    for (int d = depth - 1; d >= 0; --d) {
+        float4 s = stack[d];
+        float4 b = sc.mats[3 * __float_as_int(s.w) + 2];
+        T = f3(s.x, s.y, s.z) + f3(b.x, b.y, b.z) * T;
+    }
+    return T;
+}
+
+struct CameraDev {   // maths.h:217-224
+    F3 origin, a, u, r, llc, horiz, vert;
+    float lensRadius;
+};
+LRT_DEV Ray GetRay(const CameraDev& c, float s, float t, uint32_t& rng) {   // maths.h:205-215
+    F3 rd = c.lensRadius * RandomInUnitDisk(rng);
+    F3 offset = c.r * rd.x + c.u * rd.y;
+    return make_ray(c.origin + offset, normalize(c.llc + s * c.horiz + t * c.vert - c.origin - offset));
+}
+
+LRT_DEV uint32_t PixelSeed(uint32_t x, uint32_t y, uint32_t f) { return (x * 1973u + y * 9277u + f * 26699u) | 1u; }
+
+}  // namespace lrt

@@ -1,0 +1,417 @@
+/* TEST INFRASTRUCTURE ONLY — CPU oracle (see lrt_oracle.h for the contract).
+ *
+ * Every function cites the reference line it restates. Expressions keep the
+ * reference's association order; each float3(...) of RandomFloat01() draws is
+ * written as sequenced statements in left-to-right order.
+ * Built with -ffp-contract=off: no FMA contraction anywhere.
+ */
+#define _GNU_SOURCE
+#include "lrt_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#define kPI 3.1415926f          /* maths.h:5 */
+static const float kMinT = 0.001f;   /* parallel.cpp:9 */
+static const float kMaxT = 1.0e7f;   /* parallel.cpp:10 */
+
+typedef struct { float x, y, z; } f3;               /* maths.h:10-61 */
+typedef struct { f3 orig, dir; } ray_t;             /* maths.h:130-145 */
+typedef struct { f3 pos, normal; float t; } hit_t;  /* maths.h:148-153 */
+typedef struct { f3 center; float radius; } sphere_t;
+typedef struct { int type; f3 albedo, emissive; float roughness, ri; } mat_t;
+typedef struct { f3 origin, a, u, r, llc, horiz, vert; float lensRadius; } cam_t;
+
+static inline f3 v3(float x, float y, float z) { f3 r = {x, y, z}; return r; }
+static inline f3 add(f3 a, f3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }   /* maths.h:63 */
+static inline f3 sub(f3 a, f3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }   /* maths.h:67 */
+static inline f3 mul(f3 a, f3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }   /* maths.h:71 */
+static inline f3 mulf(f3 a, float b) { return v3(a.x * b, a.y * b, a.z * b); }     /* maths.h:75 */
+static inline f3 smul(float a, f3 b) { return v3(a * b.x, a * b.y, a * b.z); }     /* maths.h:79 */
+static inline f3 neg(f3 a) { return v3(-a.x, -a.y, -a.z); }                        /* maths.h:27 */
+static inline float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }  /* maths.h:83 */
+static inline f3 cross(f3 a, f3 b) {                                               /* maths.h:87-92 */
+    return v3(a.y * b.z - a.z * b.y, -(a.x * b.z - a.z * b.x), a.x * b.y - a.y * b.x);
+}
+static inline float length(f3 v) { return sqrtf(v.x * v.x + v.y * v.y + v.z * v.z); } /* maths.h:15 */
+static inline f3 normalize(f3 v) {                                                 /* maths.h:93-97 */
+    float k = 1.0f / length(v);
+    return v3(v.x * k, v.y * k, v.z * k);
+}
+static inline f3 normalize_member(f3 v) {                                          /* maths.h:19-25 */
+    float l = length(v);
+    return v3(v.x / l, v.y / l, v.z / l);
+}
+static inline f3 reflect(f3 v, f3 n) {                                             /* maths.h:100-103 */
+    return add(v, smul(2.0f, smul(-dot(v, n), n)));
+}
+static inline int refract(f3 v, f3 n, float nint, f3* out) {                       /* maths.h:106-118 */
+    float dt = dot(v, n);
+    float discr = 1.0f - nint * nint * (1.0f - dt * dt);
+    if (discr > 0) {
+        *out = sub(smul(nint, sub(v, mulf(n, dt))), mulf(n, sqrtf(discr)));
+        return 1;
+    }
+    return 0;
+}
+static inline float schlick(float cosine, float ri) {                              /* maths.h:122-127 */
+    float r0 = (1.0f - ri) / (1.0f + ri);
+    r0 = r0 * r0;
+    return r0 + (1.0f - r0) * powf(1.0f - cosine, 5.0f);
+}
+static inline ray_t mkray(f3 o, f3 d) { ray_t r; r.orig = o; r.dir = normalize(d); return r; } /* maths.h:133-137 */
+static inline f3 point_at(ray_t r, float t) { return add(r.orig, mulf(r.dir, t)); }          /* maths.h:139-142 */
+
+/* ---- RNG: maths.cpp:5-49, with the global state made an explicit pointer ---- */
+uint32_t orc_xorshift32(uint32_t* state) {                                        /* maths.cpp:7-15 */
+    uint32_t x = *state;
+    x ^= x << 13;
+    x ^= x >> 17;
+    x ^= x << 15;
+    *state = x;
+    return x;
+}
+float orc_random01(uint32_t* s) { return (orc_xorshift32(s) & 0xFFFFFF) / 16777216.0f; } /* maths.cpp:17-20 */
+
+static f3 random_in_unit_disk(uint32_t* s) {                                      /* maths.cpp:22-30 */
+    f3 p;
+    do {
+        float a = orc_random01(s);
+        float b = orc_random01(s);
+        p = sub(smul(2.0f, v3(a, b, 0)), v3(1, 1, 0));
+    } while (dot(p, p) >= 1.0f);
+    return p;
+}
+static f3 random_unit_vector(uint32_t* s) {                                       /* maths.cpp:32-40 */
+    float z = orc_random01(s) * 2.0f - 1.0f;
+    float a = orc_random01(s) * 2.0f * kPI;
+    float r = sqrtf(1.0f - z * z);
+    float x = r * cosf(a);
+    float y = r * sinf(a);
+    return v3(x, y, z);
+}
+static f3 random_in_unit_sphere(uint32_t* s) {                                    /* maths.cpp:42-49 */
+    f3 p;
+    do {
+        float a = orc_random01(s);
+        float b = orc_random01(s);
+        float c = orc_random01(s);
+        p = sub(smul(2.0f, v3(a, b, c)), v3(1, 1, 1));
+    } while (length(p) >= 1.0f);
+    return p;
+}
+
+static int hit_sphere(ray_t r, const sphere_t* s, float tMin, float tMax, hit_t* out) { /* maths.cpp:51-94 */
+    f3 rs = sub(s->center, r.orig);
+    float rsProj = dot(rs, r.dir);
+    float ifHit = dot(rs, rs) - rsProj * rsProj - s->radius * s->radius;
+    if (ifHit < 0.0f) {
+        float halfCut = sqrtf(-ifHit);
+        float t = rsProj - halfCut;
+        if (t > tMin && t < tMax) {
+            out->pos = point_at(r, t);
+            out->normal = normalize(sub(out->pos, s->center));
+            out->t = t;
+            return 1;
+        }
+        t = rsProj + halfCut;
+        if (t > tMin && t < tMax) {
+            out->pos = point_at(r, t);
+            out->normal = normalize(sub(out->pos, s->center));
+            out->t = t;
+            return 1;
+        }
+    }
+    return 0;
+}
+
+typedef struct {
+    const sphere_t* spheres;
+    const mat_t* mats;
+    int count;
+    int maxDepth;        /* scatter while depth < maxDepth (parallel.cpp:12,212) */
+} scene_t;
+
+static int hit_world(const scene_t* sc, ray_t r, float tMin, float tMax, hit_t* outHit, int* outID) { /* parallel.cpp:54-73 */
+    hit_t tmp;
+    int ifHit = 0;
+    float closestT = tMax;
+    for (int i = 0; i < sc->count; ++i) {
+        if (hit_sphere(r, &sc->spheres[i], tMin, closestT, &tmp)) {
+            ifHit = 1;
+            *outHit = tmp;
+            closestT = tmp.t;
+            *outID = i;
+        }
+    }
+    return ifHit;
+}
+
+static int scatter(const scene_t* sc, int matID, ray_t r_in, const hit_t* rec, f3* attenuation,
+                   ray_t* scattered, f3* outLightE, long long* rays, uint32_t* rng) {  /* parallel.cpp:78-196 */
+    const mat_t* mat = &sc->mats[matID];
+    *outLightE = v3(0, 0, 0);
+    if (mat->type == 0) {                                                          /* :81-136 */
+        f3 target = add(add(rec->pos, rec->normal), random_unit_vector(rng));
+        *scattered = mkray(rec->pos, normalize(sub(target, rec->pos)));
+        *attenuation = mat->albedo;
+        for (int i = 0; i < sc->count; ++i) {                                      /* :93-133 */
+            const mat_t* smat = &sc->mats[i];
+            if (smat->emissive.x <= 0 && smat->emissive.y <= 0 && smat->emissive.z <= 0) continue;
+            if (i == matID) continue;   /* &mat == &smat (:98): identity of the table entry */
+            const sphere_t* s = &sc->spheres[i];
+            f3 sw = normalize(sub(s->center, rec->pos));
+            f3 su = normalize(cross(fabsf(sw.x) > 0.01f ? v3(0, 1, 0) : v3(1, 0, 0), sw));
+            f3 sv = cross(sw, su);
+            float len = length(sub(rec->pos, s->center));
+            float cosAMax = sqrtf(1.0f - s->radius * s->radius / (len * len));   /* :109 */
+            float eps1 = orc_random01(rng);
+            float eps2 = orc_random01(rng);
+            float cosA = 1.0f - eps1 + eps1 * cosAMax;
+            float sinA = sqrtf(1.0f - cosA * cosA);
+            float phi = 2.0f * kPI * eps2;
+            f3 l = add(add(mulf(mulf(su, cosf(phi)), sinA), mulf(mulf(sv, sinf(phi)), sinA)),
+                       mulf(sw, cosA));                                            /* :116 */
+            l = normalize_member(l);                                               /* :117 */
+            hit_t lightHit;
+            int hitID = -1;
+            ++*rays;                                                               /* :122 */
+            if (hit_world(sc, mkray(rec->pos, l), kMinT, kMaxT, &lightHit, &hitID) && hitID == i) {
+                float omega = 2.0f * kPI * (1.0f - cosAMax);
+                f3 rdir = r_in.dir;
+                f3 nl = dot(rec->normal, rdir) < 0 ? rec->normal : neg(rec->normal);
+                float d = dot(l, nl);
+                float mx = (0.0f < d) ? d : 0.0f;                                  /* std::max(0.0f, d) */
+                *outLightE = add(*outLightE, mulf(mul(mat->albedo, smat->emissive), mx * omega / kPI));
+            }
+        }
+        return 1;
+    } else if (mat->type == 1) {                                                   /* :137-148 */
+        f3 refl = reflect(r_in.dir, rec->normal);
+        *scattered = mkray(rec->pos, normalize(add(refl, smul(mat->roughness, random_in_unit_sphere(rng)))));
+        *attenuation = mat->albedo;
+        return dot(scattered->dir, rec->normal) > 0;
+    } else if (mat->type == 2) {                                                   /* :149-193 */
+        f3 outwardN;
+        f3 rdir = r_in.dir;
+        f3 refl = reflect(rdir, rec->normal);
+        float nint;
+        f3 refr = v3(0, 0, 0);
+        float reflProb;
+        float cosine;
+        if (dot(rdir, rec->normal) > 0) {
+            outwardN = neg(rec->normal);
+            nint = mat->ri;
+            cosine = dot(rdir, rec->normal);
+        } else {
+            outwardN = rec->normal;
+            nint = 1.0f / mat->ri;
+            cosine = -dot(rdir, rec->normal);
+        }
+        if (refract(rdir, outwardN, nint, &refr))
+            reflProb = schlick(cosine, mat->ri);
+        else
+            reflProb = 1;
+        if (orc_random01(rng) < reflProb)
+            *scattered = mkray(rec->pos, normalize(refl));
+        else
+            *scattered = mkray(rec->pos, normalize(refr));
+        *attenuation = v3(1, 1, 1);
+    }
+    return 1;
+}
+
+static f3 trace(const scene_t* sc, ray_t r, int depth, long long* rays, uint32_t* rng) {   /* parallel.cpp:200-227 */
+    hit_t rec;
+    int id = 0;
+    ++*rays;
+    if (hit_world(sc, r, kMinT, kMaxT, &rec, &id)) {
+        ray_t scattered;
+        f3 attenuation, lightE;
+        f3 matE = sc->mats[id].emissive;
+        if (depth < sc->maxDepth && scatter(sc, id, r, &rec, &attenuation, &scattered, &lightE, rays, rng))
+            return add(add(matE, lightE), mul(attenuation, trace(sc, scattered, depth + 1, rays, rng)));
+        return matE;
+    }
+    f3 unitDir = r.dir;
+    float t = 0.5f * (unitDir.y + 1.0f);
+    return mulf(add(smul(1.0f - t, v3(1.0f, 1.0f, 1.0f)), smul(t, v3(0.5f, 0.7f, 1.0f))), 0.3f);
+}
+
+/* ---- camera: maths.h:183-215, DrawTest's parameters parallel.cpp:299-307 ---- */
+static cam_t make_camera(f3 lookFrom, f3 lookAt, f3 vup, float vfov, float aspect, float aperture, float focusDist) {
+    cam_t c;
+    c.lensRadius = aperture / 2.0f;
+    c.origin = lookFrom;
+    c.a = normalize(sub(lookFrom, lookAt));
+    c.r = normalize(cross(vup, c.a));
+    c.u = normalize(cross(c.a, c.r));
+    float theta = vfov * kPI / 180.0f;
+    float halfHeightTan = tanf(theta / 2.0f);
+    float halfWidthTan = aspect * halfHeightTan;
+    c.llc = sub(sub(sub(c.origin, smul(halfWidthTan * focusDist, c.r)), smul(halfHeightTan * focusDist, c.u)),
+                smul(focusDist, c.a));
+    c.horiz = smul(2.0f * halfWidthTan * focusDist, c.r);
+    c.vert = smul(2.0f * halfHeightTan * focusDist, c.u);
+    return c;
+}
+static ray_t get_ray(const cam_t* c, float s, float t, uint32_t* rng) {          /* maths.h:205-215 */
+    f3 rd = smul(c->lensRadius, random_in_unit_disk(rng));
+    f3 offset = add(mulf(c->r, rd.x), mulf(c->u, rd.y));
+    return mkray(add(c->origin, offset),
+                 normalize(sub(sub(add(add(c->llc, smul(s, c->horiz)), smul(t, c->vert)), c->origin), offset)));
+}
+static void cam_to22(const cam_t* c, float* o) {
+    const f3* v[7] = {&c->origin, &c->a, &c->u, &c->r, &c->llc, &c->horiz, &c->vert};
+    for (int i = 0; i < 7; ++i) { o[3 * i] = v[i]->x; o[3 * i + 1] = v[i]->y; o[3 * i + 2] = v[i]->z; }
+    o[21] = c->lensRadius;
+}
+static cam_t cam_from22(const float* o) {
+    cam_t c;
+    f3* v[7] = {&c.origin, &c.a, &c.u, &c.r, &c.llc, &c.horiz, &c.vert};
+    for (int i = 0; i < 7; ++i) *v[i] = v3(o[3 * i], o[3 * i + 1], o[3 * i + 2]);
+    c.lensRadius = o[21];
+    return c;
+}
+static cam_t default_camera(int w, int h) {
+    return make_camera(v3(0, 2, 3), v3(0, 0, 0), v3(0, 1, 0), 60.0f, (float)w / (float)h, 0.1f, 3.0f);
+}
+void orc_default_camera(int w, int h, float* cam22) { cam_t c = default_camera(w, h); cam_to22(&c, cam22); }
+void orc_make_camera(const float* from, const float* at, const float* up, float vfov, float aspect,
+                     float aperture, float focus, float* cam22) {
+    cam_t c = make_camera(v3(from[0], from[1], from[2]), v3(at[0], at[1], at[2]), v3(up[0], up[1], up[2]),
+                          vfov, aspect, aperture, focus);
+    cam_to22(&c, cam22);
+}
+int orc_hit_sphere(const float* o, const float* d, const float* sph, float tMin, float tMax, float* out7) {
+    ray_t r = mkray(v3(o[0], o[1], o[2]), v3(d[0], d[1], d[2]));
+    sphere_t s = {v3(sph[0], sph[1], sph[2]), sph[3]};
+    hit_t h;
+    if (!hit_sphere(r, &s, tMin, tMax, &h)) return 0;
+    out7[0] = h.pos.x; out7[1] = h.pos.y; out7[2] = h.pos.z;
+    out7[3] = h.normal.x; out7[4] = h.normal.y; out7[5] = h.normal.z; out7[6] = h.t;
+    return 1;
+}
+
+/* ---- per-pixel body of TraceRowJob (parallel.cpp:270-286) ---- */
+static inline void shade_pixel(const scene_t* sc, const cam_t* cam, int w, int h, int x, int y, int frame,
+                               uint32_t* rng, float* pix, long long* rays) {
+    float invWidth = 1.0f / (float)w;                                              /* :260 */
+    float invHeight = 1.0f / (float)h;                                             /* :261 */
+    float lerpFac = (float)frame / (float)(frame + 1);                             /* :262 */
+    float u = ((float)x + orc_random01(rng)) * invWidth;                           /* :272 */
+    float v = ((float)y + orc_random01(rng)) * invHeight;                          /* :273 */
+    ray_t r = get_ray(cam, u, v, rng);
+    f3 col = trace(sc, r, 0, rays, rng);
+    f3 prev = v3(pix[0], pix[1], pix[2]);
+    col = add(mulf(prev, lerpFac), mulf(col, 1.0f - lerpFac));                     /* :282 */
+    pix[0] = col.x;
+    pix[1] = col.y;
+    pix[2] = col.z;
+}
+
+static inline uint32_t pixel_seed(uint32_t x, uint32_t y, uint32_t f) {
+    return (x * 1973u + y * 9277u + f * 26699u) | 1u;
+}
+
+typedef struct {
+    scene_t sc;
+    cam_t cam;
+    int w, h, x0, xc, y0, yc, frame0, frames;
+    float* buf;
+    int next_row;            /* shared row cursor (atomic) */
+    long long rays;          /* per-thread slot below */
+} job_t;
+
+typedef struct { job_t* job; long long rays; } worker_t;
+
+static void* worker(void* arg) {
+    worker_t* wk = (worker_t*)arg;
+    job_t* j = wk->job;
+    for (;;) {
+        int ly = __atomic_fetch_add(&j->next_row, 1, __ATOMIC_RELAXED);
+        if (ly >= j->yc) break;
+        for (int lx = 0; lx < j->xc; ++lx) {
+            float* pix = j->buf + ((size_t)ly * j->xc + lx) * 4;
+            int x = j->x0 + lx, y = j->y0 + ly;
+            for (int f = j->frame0; f < j->frame0 + j->frames; ++f) {
+                uint32_t rng = pixel_seed((uint32_t)x, (uint32_t)y, (uint32_t)f);
+                shade_pixel(&j->sc, &j->cam, j->w, j->h, x, y, f, &rng, pix, &wk->rays);
+            }
+        }
+    }
+    return NULL;
+}
+
+static void load_scene(scene_t* sc, const float* spheres, const float* mats, int count, int depth,
+                       sphere_t** sp, mat_t** mp) {
+    *sp = (sphere_t*)malloc(sizeof(sphere_t) * (count > 0 ? count : 1));
+    *mp = (mat_t*)malloc(sizeof(mat_t) * (count > 0 ? count : 1));
+    for (int i = 0; i < count; ++i) {
+        (*sp)[i].center = v3(spheres[4 * i], spheres[4 * i + 1], spheres[4 * i + 2]);
+        (*sp)[i].radius = spheres[4 * i + 3];
+        const float* o = mats + 9 * i;
+        (*mp)[i].type = (int)o[0];
+        (*mp)[i].albedo = v3(o[1], o[2], o[3]);
+        (*mp)[i].emissive = v3(o[4], o[5], o[6]);
+        (*mp)[i].roughness = o[7];
+        (*mp)[i].ri = o[8];
+    }
+    sc->spheres = *sp;
+    sc->mats = *mp;
+    sc->count = count;
+    sc->maxDepth = depth;
+}
+
+long long orc_render_p(const float* spheres, const float* mats, int count, const float* cam22, int w, int h,
+                       int x0, int xc, int y0, int yc, int frame0, int frames, int depth, float* buf, int threads) {
+    job_t j;
+    sphere_t* sp;
+    mat_t* mp;
+    memset(&j, 0, sizeof(j));
+    load_scene(&j.sc, spheres, mats, count, depth, &sp, &mp);
+    j.cam = cam22 ? cam_from22(cam22) : default_camera(w, h);
+    j.w = w; j.h = h; j.x0 = x0; j.xc = xc; j.y0 = y0; j.yc = yc;
+    j.frame0 = frame0; j.frames = frames; j.buf = buf;
+    if (threads <= 0) threads = (int)sysconf(_SC_NPROCESSORS_ONLN);
+    if (threads < 1) threads = 1;
+    if (threads > yc) threads = yc > 0 ? yc : 1;
+    worker_t* wk = (worker_t*)calloc((size_t)threads, sizeof(worker_t));
+    pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+    for (int t = 0; t < threads; ++t) wk[t].job = &j;
+    for (int t = 1; t < threads; ++t) pthread_create(&th[t], NULL, worker, &wk[t]);
+    worker(&wk[0]);
+    long long rays = wk[0].rays;
+    for (int t = 1; t < threads; ++t) { pthread_join(th[t], NULL); rays += wk[t].rays; }
+    free(wk); free(th); free(sp); free(mp);
+    return rays;
+}
+
+long long orc_render_r(const float* spheres, const float* mats, int count, int w, int h, int frame0, int frames,
+                       int depth, uint32_t* state, float* buf) {                   /* parallel.cpp:254-294 */
+    scene_t sc;
+    sphere_t* sp;
+    mat_t* mp;
+    load_scene(&sc, spheres, mats, count, depth, &sp, &mp);
+    cam_t cam = default_camera(w, h);
+    long long rays = 0;
+    for (int f = frame0; f < frame0 + frames; ++f)
+        for (int y = 0; y < h; ++y)
+            for (int x = 0; x < w; ++x)
+                shade_pixel(&sc, &cam, w, h, x, y, f, state, buf + ((size_t)y * w + x) * 4, &rays);
+    free(sp); free(mp);
+    return rays;
+}
+
+/* glibc's own sinf / cosf / powf, in bulk: the checker for the product's libm
+ * restatement (learnraytracing_amd/csrc/lrt_libm.h). kind: 0 sinf, 1 cosf,
+ * 2 powf(x, 5), 3 powf(x, 0.416666667f) (main.cpp:112). */
+void orc_libm_eval(int kind, const float* in, float* out, long long n) {
+    for (long long i = 0; i < n; ++i) {
+        float x = in[i];
+        out[i] = kind == 0 ? sinf(x) : kind == 1 ? cosf(x) : kind == 2 ? powf(x, 5.0f) : powf(x, 0.416666667f);
+    }
+}

@@ -1,0 +1,164 @@
+"""TEST INFRASTRUCTURE ONLY — Python front end of the CPU checkers.
+
+    orc  : liblrt_oracle.so — the plain-C restatement (lrt_oracle.c), any scene size,
+           thread-safe, built anywhere with gcc (`make -C oracle`).
+    ref  : _ref/libref.so   — the reference's OWN maths.cpp/parallel.cpp compiled in
+           place (ref_harness.cpp); present only where /root/reference was available
+           at build time (travels to the GPU box as a built file). Optional.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORC_PATH = os.path.join(HERE, "liblrt_oracle.so")
+REF_PATH = os.path.join(HERE, "_ref", "libref.so")
+
+_P = ctypes.c_void_p
+_ll = ctypes.c_longlong
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(_P)
+
+
+def build_orc() -> None:
+    subprocess.run(["make", "-s", "-C", HERE, "liblrt_oracle.so"], check=True)
+
+
+_orc = None
+_ref = None
+
+
+def orc():
+    global _orc
+    if _orc is None:
+        if not os.path.exists(ORC_PATH):
+            build_orc()
+        lib = ctypes.CDLL(ORC_PATH)
+        lib.orc_render_p.restype = _ll
+        lib.orc_render_p.argtypes = [_P, _P, ctypes.c_int, _P] + [ctypes.c_int] * 9 + [_P, ctypes.c_int]
+        lib.orc_render_r.restype = _ll
+        lib.orc_render_r.argtypes = [_P, _P] + [ctypes.c_int] * 6 + [ctypes.POINTER(ctypes.c_uint32), _P]
+        lib.orc_libm_eval.restype = None
+        lib.orc_libm_eval.argtypes = [ctypes.c_int, _P, _P, _ll]
+        lib.orc_xorshift32.restype = ctypes.c_uint32
+        lib.orc_random01.restype = ctypes.c_float
+        lib.orc_default_camera.argtypes = [ctypes.c_int, ctypes.c_int, _P]
+        lib.orc_make_camera.argtypes = [_P, _P, _P, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                        ctypes.c_float, _P]
+        lib.orc_hit_sphere.argtypes = [_P, _P, _P, ctypes.c_float, ctypes.c_float, _P]
+        _orc = lib
+    return _orc
+
+
+def have_ref() -> bool:
+    return os.path.exists(REF_PATH)
+
+
+def ref():
+    global _ref
+    if _ref is None:
+        lib = ctypes.CDLL(REF_PATH)
+        for f in ("ref_render_mode_r", "ref_render_mode_p", "ref_render_mode_p_procs"):
+            getattr(lib, f).restype = _ll
+        lib.ref_render_mode_r.argtypes = [ctypes.c_int] * 5 + [_P]
+        lib.ref_render_mode_p.argtypes = [ctypes.c_int] * 9 + [_P, _P]
+        lib.ref_render_mode_p_procs.argtypes = [ctypes.c_int] * 9 + [_P, _P, ctypes.c_int]
+        lib.ref_sampler.restype = ctypes.c_uint32
+        lib.ref_get_ray.restype = ctypes.c_uint32
+        lib.ref_get_ray.argtypes = [_P, ctypes.c_uint32, ctypes.c_float, ctypes.c_float, _P]
+        lib.ref_schlick.restype = ctypes.c_float
+        lib.ref_schlick.argtypes = [ctypes.c_float, ctypes.c_float]
+        lib.ref_hit_sphere.argtypes = [_P, _P, _P, ctypes.c_float, ctypes.c_float, _P]
+        lib.ref_hit_world.argtypes = [_P, _P, ctypes.c_float, ctypes.c_float, _P]
+        lib.ref_trace.argtypes = [_P, _P, ctypes.c_int, ctypes.c_uint32, _P]
+        lib.ref_draw_test.argtypes = [ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]
+        _ref = lib
+    return _ref
+
+
+# ---- convenience wrappers ---------------------------------------------------------------
+def default_scene_arrays():
+    """The reference scene in the oracle layout, from the reference itself if built,
+    else from the restatement's constants (parallel.cpp:15-51)."""
+    s = np.array([0, -100.5, -1, 100, 2, 1, -1, .5, 0, 0, -1, .5, -2, 0, -1, .5, 2, 0, 1, .5,
+                  0, 0, 1, .5, -2, 0, 1, .5, .5, 1, .5, .5, -1.5, 1.5, 0, .3], np.float32)
+    m = np.array([0, .8, .8, .8, 0, 0, 0, 0, 0,
+                  0, .8, .4, .4, 0, 0, 0, 0, 0,
+                  0, .4, .8, .4, 0, 0, 0, 0, 0,
+                  1, .4, .4, .8, 0, 0, 0, 0, 0,
+                  1, .4, .8, .4, 0, 0, 0, 0, 0,
+                  1, .4, .8, .4, 0, 0, 0, .2, 0,
+                  1, .4, .8, .4, 0, 0, 0, .6, 0,
+                  2, .4, .4, .4, 0, 0, 0, 0, 1.5,
+                  0, .8, .6, .2, 30, 25, 15, 0, 0], np.float32)
+    return s, m
+
+
+def orc_render(width, height, frames=1, depth=8, frame0=0, x0=0, xc=None, y0=0, yc=None,
+               spheres=None, mats=None, cam22=None, buf=None, threads=0):
+    """Mode P through the C restatement. Returns (buf[yc, xc, 4], rays)."""
+    xc = width - x0 if xc is None else xc
+    yc = height - y0 if yc is None else yc
+    if spheres is None:
+        spheres, mats = default_scene_arrays()
+    spheres = np.ascontiguousarray(spheres, np.float32)
+    mats = np.ascontiguousarray(mats, np.float32)
+    if buf is None:
+        buf = np.zeros((yc, xc, 4), np.float32)
+    cam = None if cam22 is None else np.ascontiguousarray(cam22, np.float32)
+    rays = orc().orc_render_p(_ptr(spheres), _ptr(mats), len(spheres) // 4, _ptr(cam), width, height,
+                              x0, xc, y0, yc, frame0, frames, depth, _ptr(buf), threads)
+    return buf, rays
+
+
+def orc_render_r(width, height, frames=1, depth=20, frame0=0, state=1, spheres=None, mats=None):
+    """Mode R (reference stream) through the C restatement. Returns (buf, rays, end_state)."""
+    if spheres is None:
+        spheres, mats = default_scene_arrays()
+    buf = np.zeros((height, width, 4), np.float32)
+    st = ctypes.c_uint32(state)
+    rays = orc().orc_render_r(_ptr(spheres), _ptr(mats), len(spheres) // 4, width, height, frame0, frames,
+                              depth, ctypes.byref(st), _ptr(buf))
+    return buf, rays, st.value
+
+
+def orc_libm(kind: int, x: np.ndarray) -> np.ndarray:
+    x = np.ascontiguousarray(x, np.float32)
+    out = np.empty_like(x)
+    orc().orc_libm_eval(kind, _ptr(x), _ptr(out), x.size)
+    return out
+
+
+def orc_camera(width, height):
+    c = np.zeros(22, np.float32)
+    orc().orc_default_camera(width, height, _ptr(c))
+    return c
+
+
+def ref_render_p(width, height, frames=1, depth=8, frame0=0, x0=0, xc=None, y0=0, yc=None,
+                 scene=None, cam22=None, procs=1):
+    """Mode P / F through the reference itself. scene=(spheres[36], mats[81]) overrides
+    the reference's 9 statics for the call. Returns (buf, rays)."""
+    r = ref()
+    xc = width - x0 if xc is None else xc
+    yc = height - y0 if yc is None else yc
+    buf = np.zeros((yc, xc, 4), np.float32)
+    if scene is not None:
+        r.ref_set_scene(_ptr(np.ascontiguousarray(scene[0], np.float32)),
+                        _ptr(np.ascontiguousarray(scene[1], np.float32)))
+    try:
+        cam = None if cam22 is None else np.ascontiguousarray(cam22, np.float32)
+        rays = r.ref_render_mode_p_procs(width, height, x0, xc, y0, yc, frame0, frames, depth,
+                                         _ptr(cam), _ptr(buf), procs)
+    finally:
+        if scene is not None:
+            r.ref_reset_scene()
+    return buf, rays
