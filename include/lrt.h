@@ -133,7 +133,7 @@ int lrt_default_scene(lrt_sphere* spheres, lrt_material* materials, int capacity
 
 /* Render into a DEVICE buffer of row_count * x_count RGBA float quads (row-major,
  * local rows), adding the counted rays into *d_rays (device uint64, caller-zeroed).
- * Asynchronous on `stream` (a hipStream_t; NULL = the library's stream). */
+ * Asynchronous on `stream` (a hipStream_t, used as given: NULL is the default stream). */
 int lrt_render_device(const lrt_render_desc* desc, float* d_backbuffer,
                       unsigned long long* d_rays, void* stream);
 

@@ -107,6 +107,15 @@ def lib() -> ctypes.CDLL:
             if not os.path.exists(LIB_PATH):
                 raise LrtError(LRT_E_STATE, f"{LIB_PATH} is missing: run __graft_entry__.build() "
                                             "(make -C learnraytracing_amd/csrc)")
+            # One HIP runtime per process: torch ships its own libamdhip64 (DT_NEEDED
+            # "libamdhip64.so", SONAME libamdhip64.so.7). Importing torch first makes this
+            # library's DT_NEEDED libamdhip64.so.7 resolve to that same, already loaded copy;
+            # loading /opt/rocm's copy first would leave torch with a second runtime that
+            # finds no GPU.
+            try:
+                import torch  # noqa: F401
+            except ImportError:  # pragma: no cover - torch is part of the image
+                pass
             try:
                 handle = ctypes.CDLL(LIB_PATH)
             except OSError as e:   # pragma: no cover - depends on the box

@@ -467,7 +467,7 @@ int lrt_default_scene(lrt_sphere* spheres, lrt_material* materials, int capacity
 
 int lrt_render_device(const lrt_render_desc* desc, float* d_backbuffer, unsigned long long* d_rays, void* stream) {
     std::lock_guard<std::mutex> lk(g_mu);
-    return render_device(desc, d_backbuffer, d_rays, stream ? (hipStream_t)stream : g_ctx.stream);
+    return render_device(desc, d_backbuffer, d_rays, (hipStream_t)stream);
 }
 
 int lrt_render_host(const lrt_render_desc* desc, float* backbuffer, long long* out_rays) {
@@ -492,7 +492,7 @@ int lrt_unshard_rows(const float* d_src, float* d_dst, int width, int height, in
     if (!d_src || !d_dst || width < 1 || height < 1 || row_block < 1 || period < 1)
         return fail(LRT_E_INVALID, "invalid unshard arguments");
     int maxRows = lrt_shard_rows(height, row_block, period, 0);
-    hipStream_t s = stream ? (hipStream_t)stream : g_ctx.stream;
+    hipStream_t s = (hipStream_t)stream;
     dim3 grid((width + 255) / 256, height);
     unshard_kernel<<<grid, 256, 0, s>>>(reinterpret_cast<const float4*>(d_src), reinterpret_cast<float4*>(d_dst),
                                         width, height, row_block, period, maxRows);
@@ -503,7 +503,7 @@ int lrt_unshard_rows(const float* d_src, float* d_dst, int width, int height, in
 int lrt_present_bgra8(const float* d_rgba, uint32_t* d_bgra, int width, int height, void* stream) {
     if (!d_rgba || !d_bgra || width < 1 || height < 1) return fail(LRT_E_INVALID, "invalid present arguments");
     int n = width * height;
-    hipStream_t s = stream ? (hipStream_t)stream : g_ctx.stream;
+    hipStream_t s = (hipStream_t)stream;
     present_kernel<<<(n + 255) / 256, 256, 0, s>>>(reinterpret_cast<const float4*>(d_rgba), d_bgra, n);
     LRT_HIP(hipGetLastError());
     return LRT_OK;

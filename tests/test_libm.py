@@ -1,0 +1,98 @@
+"""The product's libm restatement (learnraytracing_amd/csrc/lrt_libm.h, host build via
+lrt_libm_eval_host) against glibc's own sinf/cosf/powf (the functions the reference
+calls), bit for bit. The device build is checked in tests/test_gpu_parity.py.
+
+Default runs cover the path's whole sin/cos domain (2^24 inputs) and a dense sample
+of the powf domains; LRT_EXHAUSTIVE=1 sweeps every float of [0, 1] for powf(x, 5)
+and of +/-[0, 120) for sinf/cosf (minutes)."""
+import ctypes
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from learnraytracing_amd import _lib as L
+
+
+def product(kind, x):
+    x = np.ascontiguousarray(x, np.float32)
+    out = np.empty_like(x)
+    L.check(L.lib().lrt_libm_eval_host(kind, x.ctypes.data_as(ctypes.c_void_p),
+                                       out.ctypes.data_as(ctypes.c_void_p), x.size))
+    return out
+
+
+def glibc(kind, x):
+    return oracle.orc_libm(kind, x)
+
+
+def assert_same(kind, x):
+    a, b = product(kind, x), glibc(kind, x)
+    bad = np.nonzero(a.view(np.uint32) != b.view(np.uint32))[0]
+    assert bad.size == 0, f"kind {kind}: {bad.size} mismatches, first x={x[bad[0]]!r}"
+
+
+def path_domain():
+    k = np.arange(1 << 24, dtype=np.uint32)
+    return ((np.float32(2.0) * np.float32(3.1415926)) * (k.astype(np.float32) * np.float32(2.0 ** -24))).astype(
+        np.float32)
+
+
+def test_path_domain_is_one_set():
+    """parallel.cpp:115 `2*kPI*eps2` and maths.cpp:35 `RandomFloat01()*2*kPI` produce
+    the same 2^24 floats, so one sweep covers every sin/cos call of the path."""
+    k = np.arange(0, 1 << 24, 97, dtype=np.uint32)
+    eps = (k.astype(np.float32) * np.float32(2.0 ** -24)).astype(np.float32)
+    a = ((np.float32(2.0) * np.float32(3.1415926)) * eps).astype(np.float32)
+    b = ((eps * np.float32(2.0)) * np.float32(3.1415926)).astype(np.float32)
+    assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_sincos_whole_path_domain(kind, manifest):
+    x = path_domain()
+    assert_same(kind, x)
+    key = "sinf_sha256" if kind == 0 else "cosf_sha256"
+    assert hashlib.sha256(product(kind, x).tobytes()).hexdigest() == manifest["libm"][key]
+
+
+def test_sincos_other_ranges():
+    g = np.random.default_rng(0)
+    x = np.concatenate([g.uniform(-120, 120, 1 << 20), g.uniform(-1, 1, 1 << 18),
+                        [0.0, -0.0, 1e-30, -1e-30, 2 ** -12, 2 ** -13, 0.78539816, 0.7853982, 119.9]]).astype(np.float32)
+    assert_same(0, x)
+    assert_same(1, x)
+
+
+def test_powf5_dense_and_edges(manifest):
+    u = np.arange(0, 0x3F800001, 61, dtype=np.uint32)     # every 61st float of [0, 1]
+    assert_same(2, u.view(np.float32))
+    edges = np.array([0.0, -0.0, 1.0, 1e-45, 1e-38, 1.17549435e-38, 2.0 ** -126, -1e-7, -5.96e-08,
+                      -1e-30, 1e-8, 0.999999, 3.0, 1e8, np.inf, -np.inf], np.float32)
+    assert_same(2, edges)
+    pw = np.linspace(0, 1, 1 << 20, dtype=np.float32)
+    assert hashlib.sha256(product(2, pw).tobytes()).hexdigest() == manifest["libm"]["powf5_linspace01_2p20_sha256"]
+
+
+def test_powf_srgb_exponent():
+    u = np.arange(0, np.float32(64.0).view(np.uint32), 67, dtype=np.uint32)
+    assert_same(3, u.view(np.float32))
+    assert_same(3, np.array([0.0, -0.0, 1.0, 1e-45, 1e30, 3.4e38], np.float32))
+
+
+@pytest.mark.slow
+@pytest.mark.skipif(os.environ.get("LRT_EXHAUSTIVE") != "1", reason="set LRT_EXHAUSTIVE=1")
+def test_exhaustive_sweeps():
+    step = 1 << 24
+    for lo in range(0, 0x3F800001, step):
+        u = np.arange(lo, min(lo + step, 0x3F800001), dtype=np.uint32)
+        assert_same(2, u.view(np.float32))
+    top = np.float32(120.0).view(np.uint32)
+    for lo in range(0, int(top), step):
+        u = np.arange(lo, min(lo + step, int(top)), dtype=np.uint32)
+        for sgn in (0, 0x80000000):
+            x = (u | np.uint32(sgn)).view(np.float32)
+            assert_same(0, x)
+            assert_same(1, x)

@@ -1,0 +1,108 @@
+"""The CPU oracle (oracle/lrt_oracle.c) against the golden vectors generated from the
+reference itself (tests/golden/make_golden.py): KATs, the reference stream (Mode R,
+config 1), per-pixel-seeded frames (Mode P) and fuzzed scenes (Mode F). Bit-exact."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle
+
+P = oracle._ptr
+
+
+def test_xorshift_and_random01_kat(kat):
+    o = oracle.orc()
+    st = ctypes.c_uint32(1)
+    assert [o.orc_xorshift32(ctypes.byref(st)) for _ in range(16)] == kat["xorshift32_from_1"]
+    st = ctypes.c_uint32(1)
+    got = np.array([o.orc_random01(ctypes.byref(st)) for _ in range(16)], np.float32)
+    assert np.array_equal(got, np.array(kat["random01_from_1"], np.float32))
+    # SURVEY §8(c) KAT
+    assert kat["xorshift32_from_1"][:5] == [268476417, 1157628417, 1158709409, 269814307, 672445067]
+
+
+def test_default_camera_kat(kat):
+    for key, want in kat["default_camera"].items():
+        w, h = (int(v) for v in key.split("x"))
+        assert np.array_equal(oracle.orc_camera(w, h), np.array(want, np.float32)), key
+    # LLC (-3.07920098, -1.10525393, 1.46461773), H (6.15840197, 0, 0)
+    c = oracle.orc_camera(1280, 720)
+    assert np.allclose(c[12:15], [-3.07920098, -1.10525393, 1.46461773], atol=0, rtol=1e-7)
+
+
+def test_hit_sphere_kat(kat):
+    o = oracle.orc()
+    for case in kat["hit_sphere"]:
+        out = np.zeros(7, np.float32)
+        hit = o.orc_hit_sphere(P(np.array(case["o"], np.float32)), P(np.array(case["d"], np.float32)),
+                               P(np.array(case["sphere"], np.float32)), case["tmin"], case["tmax"], P(out))
+        assert hit == case["hit"]
+        if hit:
+            assert np.array_equal(out, np.array(case["out"], np.float32))
+    # main.cpp:215-226: ray from the origin along -z vs the sphere at the origin, r 0.5
+    first = kat["hit_sphere"][0]
+    assert first["hit"] == 1 and first["out"][6] == 0.5 and first["out"][3:6] == [0.0, 0.0, -1.0]
+
+
+def test_mode_r_config1(manifest, images):
+    """Config 1: the reference as written (global RNG, rows in order, kMaxDepth 20)."""
+    fx = manifest["fixtures"]["mode_r_320x180"]
+    buf, rays, _ = oracle.orc_render_r(320, 180)
+    assert rays == fx["rays"] == 183124
+    assert np.array_equal(buf[..., :3], images["mode_r_320x180"])
+    import hashlib
+    assert hashlib.md5(buf.tobytes()).hexdigest() == fx["md5_rgba"] == "ec736ffc672148552d39a532024455d7"
+
+
+@pytest.mark.parametrize("name", ["p_160x90_s4_d8", "p_320x180_s4_d8", "p_96x54_s1_d50", "p_128x72_s2_d20",
+                                  "p_128x72_f5_s3_d8", "c2_crop", "c3_crop", "c5_crop"])
+def test_mode_p(manifest, images, name):
+    fx = manifest["fixtures"][name]
+    buf, rays = oracle.orc_render(fx["w"], fx["h"], fx["frames"], fx["max_depth"], fx["frame0"], fx["x0"],
+                                  fx["xc"], fx["y0"], fx["yc"])
+    assert rays == fx["rays"]
+    assert np.array_equal(buf[..., :3].view(np.uint32), images[name].view(np.uint32))
+
+
+def test_mode_f_fuzz(manifest, images):
+    for fz in manifest["fuzz"]:
+        buf, rays = oracle.orc_render(fz["w"], fz["h"], fz["frames"], fz["max_depth"],
+                                      spheres=np.array(fz["spheres"], np.float32),
+                                      mats=np.array(fz["mats"], np.float32), cam22=np.array(fz["camera"], np.float32))
+        assert rays == fz["rays"], fz["name"]
+        assert np.array_equal(buf[..., :3].view(np.uint32), images[fz["name"]].view(np.uint32)), fz["name"]
+
+
+def test_fuzz_covers_every_material_and_tir(manifest):
+    types = set()
+    max_ri = 0.0
+    for fz in manifest["fuzz"]:
+        m = np.array(fz["mats"]).reshape(9, 9)
+        types |= set(m[:, 0].astype(int).tolist())
+        max_ri = max(max_ri, m[:, 8].max())
+    assert types == {0, 1, 2} and max_ri > 1.5
+
+
+@pytest.mark.parametrize("name", ["scene1000_c4_crop", "scene1000_c5_crop"])
+def test_scene1000_crops(manifest, images, name):
+    from learnraytracing_amd.scene import random_scene, scene_arrays
+    fx = manifest["fixtures"][name]
+    s, m = (np.array(v, np.float32) for v in scene_arrays(*random_scene(1000, 1)))
+    buf, rays = oracle.orc_render(fx["w"], fx["h"], fx["frames"], fx["max_depth"], 0, fx["x0"], fx["xc"],
+                                  fx["y0"], fx["yc"], spheres=s, mats=m)
+    assert rays == fx["rays"]
+    assert np.array_equal(buf[..., :3].view(np.uint32), images[name].view(np.uint32))
+
+
+def test_thread_count_does_not_change_output():
+    a, ra = oracle.orc_render(96, 54, 2, 8, threads=1)
+    b, rb = oracle.orc_render(96, 54, 2, 8, threads=5)
+    assert ra == rb and np.array_equal(a, b)
+
+
+def test_empty_and_ragged_windows():
+    buf, rays = oracle.orc_render(64, 36, 1, 8, x0=63, xc=1, y0=35, yc=1)
+    assert buf.shape == (1, 1, 4) and rays > 0
+    buf, rays = oracle.orc_render(64, 36, 0, 8)
+    assert rays == 0 and not buf.any()

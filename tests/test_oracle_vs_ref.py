@@ -1,0 +1,38 @@
+"""Live pinning of the C restatement against the reference itself (oracle/_ref, built
+from /root/reference in the build container; skipped where it is absent)."""
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.skipif(not oracle.have_ref(), reason="oracle/_ref/libref.so not built")
+
+
+def test_mode_r_two_frames():
+    r = oracle.ref()
+    w, h = 160, 90
+    a = np.zeros((h, w, 4), np.float32)
+    ra = r.ref_render_mode_r(w, h, 0, 2, 1, oracle._ptr(a))
+    b, rb, _ = oracle.orc_render_r(w, h, frames=2)
+    assert ra == rb and np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("seed", range(20, 32))
+def test_fresh_fuzz_scenes(seed):
+    import sys
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_golden import fuzz_scene
+    import ctypes
+    s, m = fuzz_scene(seed)
+    depth = [8, 20, 50][seed % 3]
+    a, ra = oracle.ref_render_p(48, 27, 2, depth, frame0=seed, scene=(s, m))
+    b, rb = oracle.orc_render(48, 27, 2, depth, frame0=seed, spheres=s, mats=m)
+    assert ra == rb and np.array_equal(a, b)
+    del ctypes
+
+
+def test_config2_full_frame():
+    a, ra = oracle.ref_render_p(1280, 720, 4, 8, procs=8)
+    b, rb = oracle.orc_render(1280, 720, 4, 8)
+    assert ra == rb == 11669343 and np.array_equal(a, b)
