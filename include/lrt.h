@@ -95,6 +95,8 @@ typedef struct lrt_render_desc {
 
 #define LRT_F_NONE 0
 #define LRT_F_SCENE_GLOBAL 1 /* read the scene from global memory instead of LDS staging */
+#define LRT_F_SIMPLE 2       /* v0 kernel: one work-item per pixel for all its samples
+                                (reference-shaped, for A/B and cross-checking)         */
 
 /* ---- the reference API (parallel.h:6-8) ---------------------------------- */
 

@@ -24,6 +24,7 @@ LAMBERT, METAL, DIELECTRIC = 0, 1, 2          # parallel.cpp:31
 REFERENCE_MAX_DEPTH = 20                      # parallel.cpp:12
 MAX_SPHERES = 4096
 F_SCENE_GLOBAL = 1
+F_SIMPLE = 2
 
 
 class LrtError(RuntimeError):

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "lrt.h"
+#include "lrt_paths.h"
 #include "lrt_trace.h"
 
 #define LRT_VERSION_STRING "lrt-mi355x 0.1.0 gfx950"
@@ -134,9 +135,15 @@ __global__ void libm_kernel(int kind, const float* __restrict__ in, float* __res
 
 // ---------------------------------------------------------------------------------
 // host side
+constexpr int kQueueSlots = 64;
+constexpr int kLdsLevels = 8;
+
 struct Context {
     bool ready = false;
     int device = 0;
+    int num_cus = 0;
+    unsigned int* d_queue = nullptr;   // kQueueSlots work counters, one per in-flight launch
+    unsigned queue_next = 0;
     hipStream_t stream = nullptr;
     int count = 0, nlights = 0;
     float4* d_sph = nullptr;
@@ -273,6 +280,38 @@ hipError_t launch_depth(const KernelArgs& a, bool lds, dim3 grid, hipStream_t s)
     return hipGetLastError();
 }
 
+template <bool kLdsScene>
+int launch_paths(PathArgs& a, hipStream_t s) {
+    const size_t lds = sizeof(float4) * ((size_t)kLdsLevels * kPathBlock + (kLdsScene ? a.count : 0));
+    int per_cu = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, paths_kernel<kLdsLevels, kLdsScene>,
+                                                                kPathBlock, lds);
+    if (e != hipSuccess) return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
+    if (per_cu < 1) return fail(LRT_E_INVALID, "paths_kernel does not fit on a CU (scene too large for LDS)");
+    long long want = ((long long)a.nitems + kPathBlock - 1) / kPathBlock;
+    long long blocks = (long long)per_cu * g_ctx.num_cus;
+    if (blocks > want) blocks = want;
+    const size_t gthreads = (size_t)blocks * kPathBlock;
+    float4* overflow = nullptr;
+    if (a.maxDepth > kLdsLevels) {
+        e = hipMallocAsync((void**)&overflow, sizeof(float4) * gthreads * (size_t)(a.maxDepth - kLdsLevels), s);
+        if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(path stack overflow)");
+    }
+    a.overflow = overflow;
+    unsigned int* q = g_ctx.d_queue + (g_ctx.queue_next++ % kQueueSlots);
+    a.queue = q;
+    e = hipMemsetAsync(q, 0, sizeof(unsigned int), s);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(queue)");
+    paths_kernel<kLdsLevels, kLdsScene><<<dim3((unsigned)blocks), kPathBlock, lds, s>>>(a);
+    e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "paths_kernel launch");
+    if (overflow) {
+        e = hipFreeAsync(overflow, s);
+        if (e != hipSuccess) return hip_fail(e, "hipFreeAsync(path stack overflow)");
+    }
+    return LRT_OK;
+}
+
 int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_rays, hipStream_t s) {
     int rc = validate(d);
     if (rc) return rc;
@@ -309,6 +348,31 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     a.out = reinterpret_cast<float4*>(d_buf);
     a.rays = d_rays;
     const bool lds = !(d->flags & LRT_F_SCENE_GLOBAL) && a.count <= kLdsSphereLimit;
+    if (!(d->flags & LRT_F_SIMPLE)) {
+        PathArgs p;
+        p.cam = a.cam;
+        p.sph = a.sph;
+        p.mats = a.mats;
+        p.lights = a.lights;
+        p.count = a.count;
+        p.nlights = a.nlights;
+        p.width = a.width;
+        p.height = a.height;
+        p.x0 = a.x0;
+        p.xc = a.xc;
+        p.y0 = a.y0;
+        p.rows = a.rows;
+        p.rb = a.rb;
+        p.rp = a.rp;
+        p.rph = a.rph;
+        p.frame0 = a.frame0;
+        p.frames = a.frames;
+        p.maxDepth = a.maxDepth;
+        p.nitems = a.xc * a.rows;
+        p.out = a.out;
+        p.rays = a.rays;
+        return lds ? launch_paths<true>(p, s) : launch_paths<false>(p, s);
+    }
     dim3 grid((d->x_count + kTileX - 1) / kTileX, (d->row_count + kTileY - 1) / kTileY);
     hipError_t e;
     if (d->max_depth <= 8)
@@ -397,6 +461,8 @@ int lrt_initialize(void) {
     g_ctx.device = dev;
     LRT_HIP(hipStreamCreateWithFlags(&g_ctx.stream, hipStreamNonBlocking));
     LRT_HIP(hipMalloc(&g_ctx.d_rays, sizeof(unsigned long long)));
+    LRT_HIP(hipMalloc(&g_ctx.d_queue, sizeof(unsigned int) * kQueueSlots));
+    LRT_HIP(hipDeviceGetAttribute(&g_ctx.num_cus, hipDeviceAttributeMultiprocessorCount, dev));
     int rc = upload_scene(g_ctx, kDefaultSpheres, kDefaultMats, 9);
     if (rc) return rc;
     g_ctx.ready = true;
@@ -410,6 +476,7 @@ int lrt_shutdown(void) {
     free_scene(g_ctx);
     if (g_ctx.d_frame) (void)hipFree(g_ctx.d_frame);
     if (g_ctx.d_rays) (void)hipFree(g_ctx.d_rays);
+    if (g_ctx.d_queue) (void)hipFree(g_ctx.d_queue);
     if (g_ctx.stream) (void)hipStreamDestroy(g_ctx.stream);
     g_ctx = Context();
     return LRT_OK;

@@ -120,6 +120,31 @@ LRT_HD float cosf(float y) {
     return sinf_poly(x * s, x * x, sincos_poly((n & 2) ? 1 : 0), n ^ 1);
 }
 
+// sinf and cosf of the same argument with one shared reduction (glibc's sincosf
+// computes both exactly like this, and each result has the bits of the single call).
+LRT_HD void sincosf(float y, float* sinp, float* cosp) {
+    double x = y;
+    if (abstop12(y) < abstop12(0x1.921FB6p-1f)) {
+        if (abstop12(y) < abstop12(0x1p-12f)) {
+            *sinp = y;
+            *cosp = 1.0f;
+            return;
+        }
+        const SinCosPoly p = sincos_poly(0);
+        const double x2 = x * x;
+        *sinp = sinf_poly(x, x2, p, 0);
+        *cosp = sinf_poly(x, x2, p, 1);
+        return;
+    }
+    int n;
+    x = reduce_fast(x, &n);
+    const double s = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;
+    const SinCosPoly p = sincos_poly((n & 2) ? 1 : 0);
+    const double xs = x * s, x2 = x * x;
+    *sinp = sinf_poly(xs, x2, p, n);
+    *cosp = sinf_poly(xs, x2, p, n ^ 1);
+}
+
 // ---- powf: powf_log2_data.c (POWF_LOG2_TABLE_BITS 4, POWF_SCALE_BITS 0) ----
 LRT_CONST double kPowLog2InvC[16] = {
     0x1.661ec79f8f3bep+0, 0x1.571ed4aaf883dp+0, 0x1.49539f0f010b0p+0, 0x1.3c995b0b80385p+0,

@@ -87,8 +87,10 @@ LRT_DEV F3 RandomUnitVector(uint32_t& s) {
     float z = RandomFloat01(s) * 2.0f - 1.0f;
     float a = RandomFloat01(s) * 2.0f * kPI;
     float r = __builtin_sqrtf(1.0f - z * z);
-    float x = r * libm::cosf(a);
-    float y = r * libm::sinf(a);
+    float sa, ca;
+    libm::sincosf(a, &sa, &ca);   // bit-identical to separate cosf(a), sinf(a)
+    float x = r * ca;
+    float y = r * sa;
     return f3(x, y, z);
 }
 LRT_DEV F3 RandomInUnitSphere(uint32_t& s) {
