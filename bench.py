@@ -115,6 +115,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=None, help="seconds of CPU-baseline timing")
     ap.add_argument("--scene-global", action="store_true", help="read spheres from global memory, not LDS")
+    ap.add_argument("--kernel", choices=["v0", "v1"], default="v1",
+                    help="v1: path-regeneration megakernel (default); v0: one work-item per pixel (LRT_F_SIMPLE)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -152,7 +154,7 @@ def main():
     rb = H if world == 1 else args.row_block
     max_rows = max_shard_rows(H, rb, world)
     rows = shard_rows(H, rb, world, rank)
-    flags = 1 if args.scene_global else 0
+    flags = (1 if args.scene_global else 0) | (2 if args.kernel == "v0" else 0)
     job = lrt.Job(width=W, height=H, frame0=0, frames=spp_total, max_depth=D, row_block=rb,
                   row_period=world, row_phase=rank, row_count=rows, flags=flags)
     dev = torch.device("cuda", local_rank)
@@ -250,6 +252,7 @@ def main():
                 "parallelism": f"rows: row-block-cyclic x{world} (block {rb}), RCCL gather to rank 0"
                 if world > 1 else "single GPU",
                 "scene_reads": "global" if args.scene_global else "LDS-staged",
+                "kernel": args.kernel,
             },
             "roofline": {
                 "bound": "hbm",
@@ -258,7 +261,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6),
                 "traffic": traffic,
-                "kernel": "trace_kernel",
+                "kernel": "paths_kernel" if args.kernel == "v1" else "trace_kernel",
                 "kernel_ms": round(kernel_ms, 4),
                 "algorithmic_bytes_per_launch": alg_bytes,
                 "note": "24 B per pixel-sample (SURVEY 8(d)); the path is VALU-bound, HBM frac is "

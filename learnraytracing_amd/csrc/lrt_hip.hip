@@ -282,7 +282,7 @@ hipError_t launch_depth(const KernelArgs& a, bool lds, dim3 grid, hipStream_t s)
 
 template <bool kLdsScene>
 int launch_paths(PathArgs& a, hipStream_t s) {
-    const size_t lds = sizeof(float4) * ((size_t)kLdsLevels * kPathBlock + (kLdsScene ? a.count : 0));
+    const size_t lds = paths_lds_bytes(kLdsLevels, kLdsScene, a.count, a.nlights);
     int per_cu = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, paths_kernel<kLdsLevels, kLdsScene>,
                                                                 kPathBlock, lds);
@@ -371,7 +371,11 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
         p.nitems = a.xc * a.rows;
         p.out = a.out;
         p.rays = a.rays;
-        return lds ? launch_paths<true>(p, s) : launch_paths<false>(p, s);
+        // the whole scene (spheres, materials, lights) is staged in LDS when it fits
+        // next to the stack with room for 2 blocks per CU; otherwise it is read from global
+        const bool lds_scene = !(d->flags & LRT_F_SCENE_GLOBAL) &&
+                               2 * paths_lds_bytes(kLdsLevels, true, a.count, a.nlights) <= 160 * 1024;
+        return lds_scene ? launch_paths<true>(p, s) : launch_paths<false>(p, s);
     }
     dim3 grid((d->x_count + kTileX - 1) / kTileX, (d->row_count + kTileY - 1) / kTileY);
     hipError_t e;

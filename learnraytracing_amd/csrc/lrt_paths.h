@@ -55,8 +55,10 @@ struct PathArgs {
 LRT_DEV int ClosestHit(const F3& o, const F3& d, const float4* sph, int count, float& tOut) {
     float closestT = kMaxT;
     int id = -1;
+    float4 next = sph[0];
     for (int i = 0; i < count; ++i) {
-        const float4 s = sph[i];
+        const float4 s = next;
+        if (i + 1 < count) next = sph[i + 1];   // issue the next sphere's read before this test
         const F3 rs = f3(s.x, s.y, s.z) - o;
         const float rsProj = dot(rs, d);
         const float ifHit = dot(rs, rs) - rsProj * rsProj - s.w;
@@ -110,6 +112,14 @@ struct PathStack {
     }
 };
 
+// LDS carve-up of paths_kernel: [stack kLdsLevels x 256][spheres N][materials 3N][lights]
+// (kLdsScene; otherwise only the stack is in LDS and the scene is read from global).
+__host__ __device__ inline size_t paths_lds_bytes(int lds_levels, bool lds_scene, int count, int nlights) {
+    size_t b = sizeof(float4) * (size_t)lds_levels * kPathBlock;
+    if (lds_scene) b += sizeof(float4) * 4 * (size_t)count + sizeof(int) * (size_t)(nlights > 0 ? nlights : 1);
+    return b;
+}
+
 template <int kLdsLevels, bool kLdsScene>
 __global__ __launch_bounds__(kPathBlock) void paths_kernel(const PathArgs a) {
     extern __shared__ float4 smem[];
@@ -122,13 +132,20 @@ __global__ __launch_bounds__(kPathBlock) void paths_kernel(const PathArgs a) {
     stk.gtid = (size_t)blockIdx.x * kPathBlock + tid;
     stk.gthreads = (size_t)gridDim.x * kPathBlock;
     const float4* sph = a.sph;
+    const float4* mats = a.mats;
+    const int* lights = a.lights;
     if (kLdsScene) {
         float4* s_sph = smem + kLdsLevels * kPathBlock;
+        float4* s_mat = s_sph + a.count;
+        int* s_lights = reinterpret_cast<int*>(s_mat + 3 * a.count);
         for (int i = tid; i < a.count; i += kPathBlock) s_sph[i] = a.sph[i];
+        for (int i = tid; i < 3 * a.count; i += kPathBlock) s_mat[i] = a.mats[i];
+        for (int i = tid; i < a.nlights; i += kPathBlock) s_lights[i] = a.lights[i];
         __syncthreads();
         sph = s_sph;
+        mats = s_mat;
+        lights = s_lights;
     }
-    const float4* __restrict__ mats = a.mats;
     const float invWidth = 1.0f / (float)a.width;     // parallel.cpp:260
     const float invHeight = 1.0f / (float)a.height;   // parallel.cpp:261
     const int fend = a.frame0 + a.frames;
@@ -146,9 +163,9 @@ __global__ __launch_bounds__(kPathBlock) void paths_kernel(const PathArgs a) {
     // ray; when no light is left, push (matE + lightE, self) and continue the path along
     // the scattered direction.
     auto next_light = [&]() {
-        while (k < a.nlights && a.lights[k] == self) ++k;
+        while (k < a.nlights && lights[k] == self) ++k;
         if (k < a.nlights) {
-            lid = a.lights[k];
+            lid = lights[k];
             const float4 s = sph[lid];
             const F3 c = f3(s.x, s.y, s.z);
             const F3 sw = normalize(c - o);
@@ -243,6 +260,7 @@ __global__ __launch_bounds__(kPathBlock) void paths_kernel(const PathArgs a) {
         if (kind != kDead) id = ClosestHit(o, d, sph, a.count, t);
 
         // ---- (D) state update -------------------------------------------------------
+        bool wantLight = false;
         if (kind == kShadow) {
             if (id == lid) {                                                     // :123
                 const float4 e = mats[3 * lid + 1];
@@ -250,7 +268,7 @@ __global__ __launch_bounds__(kPathBlock) void paths_kernel(const PathArgs a) {
                 lightE = lightE + (f3(alb.x, alb.y, alb.z) * f3(e.x, e.y, e.z)) * w;   // :131
             }
             ++k;
-            next_light();
+            wantLight = true;
         } else if (kind == kBounce) {
             bool finish = false;
             F3 leaf;
@@ -272,7 +290,7 @@ __global__ __launch_bounds__(kPathBlock) void paths_kernel(const PathArgs a) {
                         self = id;
                         o = pos;
                         k = 0;
-                        next_light();
+                        wantLight = true;
                     } else if (mat.type == 1) {                                  // Metal :137-148
                         const F3 refl = reflect(d, normal);
                         const F3 nd = normalize(normalize(refl + mat.roughness * RandomInUnitSphere(rng)));
@@ -338,6 +356,7 @@ __global__ __launch_bounds__(kPathBlock) void paths_kernel(const PathArgs a) {
                 kind = kNeed;
             }
         }
+        if (wantLight) next_light();   // the one call site: shadow follow-up or new Lambert hit
     }
     unsigned long long total = (unsigned long long)rays;
     for (int off = 32; off > 0; off >>= 1) total += __shfl_xor(total, off, 64);
