@@ -92,6 +92,12 @@ def cpu_baseline(cfg, budget_s: float):
                       f"{rays} rays in {dt:.2f} s, {cores} {'processes' if use_ref else 'threads'}; {src}"}
 
 
+def kernel_name(kernel: str, frames: int) -> str:
+    if kernel == "auto":   # mirrors render_device's policy in lrt_hip.hip
+        kernel = "v2s" if frames >= 8 else "v0"
+    return {"v0": "trace_kernel", "v1": "paths_kernel"}.get(kernel, "paths2_kernel")
+
+
 def read_traffic(cfg_name: str):
     """HBM bytes per launch of trace_kernel from the committed PMC run, if any."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -115,8 +121,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=None, help="seconds of CPU-baseline timing")
     ap.add_argument("--scene-global", action="store_true", help="read spheres from global memory, not LDS")
-    ap.add_argument("--kernel", choices=["v0", "v1"], default="v1",
-                    help="v1: path-regeneration megakernel (default); v0: one work-item per pixel (LRT_F_SIMPLE)")
+    ap.add_argument("--kernel", choices=["auto", "v0", "v1", "v2", "v2s", "v2s2", "v2s4"], default="auto",
+                    help="auto: the library's policy (default); v0: one pixel per lane (LRT_F_SIMPLE); "
+                         "v1: unscheduled state machine; v2: phase-scheduled persistent; v2s[N]: "
+                         "phase-scheduled, N static pixels per lane")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -154,7 +162,7 @@ def main():
     rb = H if world == 1 else args.row_block
     max_rows = max_shard_rows(H, rb, world)
     rows = shard_rows(H, rb, world, rank)
-    flags = (1 if args.scene_global else 0) | (2 if args.kernel == "v0" else 0)
+    flags = (1 if args.scene_global else 0) | {"auto": 0, "v0": 2, "v1": 4, "v2": 16, "v2s": 8, "v2s2": 8 | 2 << 8, "v2s4": 8 | 4 << 8}[args.kernel]
     job = lrt.Job(width=W, height=H, frame0=0, frames=spp_total, max_depth=D, row_block=rb,
                   row_period=world, row_phase=rank, row_count=rows, flags=flags)
     dev = torch.device("cuda", local_rank)
@@ -261,7 +269,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6),
                 "traffic": traffic,
-                "kernel": "paths_kernel" if args.kernel == "v1" else "trace_kernel",
+                "kernel": kernel_name(args.kernel, spp_total),
                 "kernel_ms": round(kernel_ms, 4),
                 "algorithmic_bytes_per_launch": alg_bytes,
                 "note": "24 B per pixel-sample (SURVEY 8(d)); the path is VALU-bound, HBM frac is "

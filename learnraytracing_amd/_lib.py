@@ -11,7 +11,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liblrt_hip.so")
+# LRT_LIB overrides the library path (development A/B builds only)
+LIB_PATH = os.environ.get("LRT_LIB") or os.path.join(_HERE, "liblrt_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "lrt.h")
 
 LRT_OK = 0
@@ -25,6 +26,9 @@ REFERENCE_MAX_DEPTH = 20                      # parallel.cpp:12
 MAX_SPHERES = 4096
 F_SCENE_GLOBAL = 1
 F_SIMPLE = 2
+F_V1 = 4
+F_V2S = 8
+F_V2 = 16
 
 
 class LrtError(RuntimeError):

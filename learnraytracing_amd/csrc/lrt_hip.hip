@@ -17,6 +17,7 @@
 
 #include "lrt.h"
 #include "lrt_paths.h"
+#include "lrt_paths2.h"
 #include "lrt_trace.h"
 
 #define LRT_VERSION_STRING "lrt-mi355x 0.1.0 gfx950"
@@ -27,7 +28,6 @@ constexpr int kTileX = 16;
 constexpr int kTileY = 16;
 constexpr int kBlock = kTileX * kTileY;  // 4 waves
 constexpr int kMaxDepthSupported = 64;
-constexpr int kLdsSphereLimit = 4096;     // 64 KiB of float4
 
 struct KernelArgs {
     CameraDev cam;
@@ -48,18 +48,27 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
     return v;
 }
 
+#ifndef LRT_WAVES_PER_EU
+#define LRT_WAVES_PER_EU 1
+#endif
 template <int MAXD, bool kLds>
-__global__ __launch_bounds__(kBlock) void trace_kernel(const KernelArgs a) {
-    extern __shared__ float4 s_sph[];
+__global__ __launch_bounds__(kBlock, LRT_WAVES_PER_EU) void trace_kernel(const KernelArgs a) {
+    // LDS: [recursion stack kTraceLdsLevels x kBlock][spheres][materials][lights]
+    extern __shared__ float4 smem[];
     const int tid = threadIdx.x;
+    float4* s_sph = smem + kTraceLdsLevels * kBlock;
+    float4* s_mat = s_sph + a.count;
+    int* s_lights = reinterpret_cast<int*>(s_mat + 3 * a.count);
     if (kLds) {
         for (int i = tid; i < a.count; i += kBlock) s_sph[i] = a.sph[i];
+        for (int i = tid; i < 3 * a.count; i += kBlock) s_mat[i] = a.mats[i];
+        for (int i = tid; i < a.nlights; i += kBlock) s_lights[i] = a.lights[i];
         __syncthreads();
     }
     SceneView sc;
     sc.sph = kLds ? s_sph : a.sph;
-    sc.mats = a.mats;
-    sc.lights = a.lights;
+    sc.mats = kLds ? s_mat : a.mats;
+    sc.lights = kLds ? s_lights : a.lights;
     sc.count = a.count;
     sc.nlights = a.nlights;
 
@@ -81,7 +90,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KernelArgs a) {
             float u = ((float)x + RandomFloat01(rng)) * invWidth;              // :272
             float v = ((float)y + RandomFloat01(rng)) * invHeight;             // :273
             Ray r = GetRay(a.cam, u, v, rng);
-            F3 col = Trace<MAXD>(r, a.maxDepth, rays, rng, sc);
+            F3 col = Trace<MAXD>(r, a.maxDepth, rays, rng, sc, smem + tid, kBlock);
             F3 prev = f3(acc.x, acc.y, acc.z);
             col = prev * lerpFac + col * (1.0f - lerpFac);                     // :282
             acc.x = col.x;
@@ -272,25 +281,34 @@ int validate(const lrt_render_desc* d) {
 
 template <int MAXD>
 hipError_t launch_depth(const KernelArgs& a, bool lds, dim3 grid, hipStream_t s) {
+    const size_t stack = sizeof(float4) * kTraceLdsLevels * kBlock;
     if (lds) {
-        trace_kernel<MAXD, true><<<grid, kBlock, sizeof(float4) * a.count, s>>>(a);
+        const size_t scene = sizeof(float4) * (4 * (size_t)a.count + (size_t)(a.nlights + 3) / 4 + 1);
+        trace_kernel<MAXD, true><<<grid, kBlock, stack + scene, s>>>(a);
     } else {
-        trace_kernel<MAXD, false><<<grid, kBlock, 0, s>>>(a);
+        trace_kernel<MAXD, false><<<grid, kBlock, stack, s>>>(a);
     }
     return hipGetLastError();
 }
 
-template <bool kLdsScene>
+template <bool kLdsScene, bool kV2, bool kOverflow, int kPix = 0>
 int launch_paths(PathArgs& a, hipStream_t s) {
-    const size_t lds = paths_lds_bytes(kLdsLevels, kLdsScene, a.count, a.nlights);
+    constexpr bool kStaticPixel = kPix > 0;
+    const size_t lds = paths_lds_bytes(kLdsLevels, kLdsScene, a.count, a.nlights, kPix);
     int per_cu = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, paths_kernel<kLdsLevels, kLdsScene>,
-                                                                kPathBlock, lds);
+    const void* kern = kV2 ? (const void*)paths2_kernel<kLdsLevels, kLdsScene, kOverflow, kPix>
+                           : (const void*)paths_kernel<kLdsLevels, kLdsScene>;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kPathBlock, lds);
     if (e != hipSuccess) return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
     if (per_cu < 1) return fail(LRT_E_INVALID, "paths_kernel does not fit on a CU (scene too large for LDS)");
     long long want = ((long long)a.nitems + kPathBlock - 1) / kPathBlock;
     long long blocks = (long long)per_cu * g_ctx.num_cus;
     if (blocks > want) blocks = want;
+    dim3 grid((unsigned)blocks);
+    if (kStaticPixel) {   // one pixel per lane: 16x16 tiles, no persistence
+        grid = dim3((unsigned)((a.xc + 15) / 16), (unsigned)((a.rows + 16 * kPix - 1) / (16 * kPix)));
+        blocks = (long long)grid.x * grid.y;
+    }
     const size_t gthreads = (size_t)blocks * kPathBlock;
     float4* overflow = nullptr;
     if (a.maxDepth > kLdsLevels) {
@@ -298,13 +316,35 @@ int launch_paths(PathArgs& a, hipStream_t s) {
         if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(path stack overflow)");
     }
     a.overflow = overflow;
+    a.stamps = nullptr;
+#ifdef LRT_EXP_STAMPS
+    static unsigned long long* d_stamps = nullptr;
+    if (!d_stamps) (void)hipMalloc(&d_stamps, sizeof(unsigned long long) * 3 * (kSecCount + 1));
+    (void)hipMemsetAsync(d_stamps, 0, sizeof(unsigned long long) * 3 * (kSecCount + 1), s);
+    a.stamps = d_stamps;
+#endif
     unsigned int* q = g_ctx.d_queue + (g_ctx.queue_next++ % kQueueSlots);
     a.queue = q;
     e = hipMemsetAsync(q, 0, sizeof(unsigned int), s);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(queue)");
-    paths_kernel<kLdsLevels, kLdsScene><<<dim3((unsigned)blocks), kPathBlock, lds, s>>>(a);
+    if (kV2)
+        paths2_kernel<kLdsLevels, kLdsScene, kOverflow, kPix><<<grid, kPathBlock, lds, s>>>(a);
+    else
+        paths_kernel<kLdsLevels, kLdsScene><<<dim3((unsigned)blocks), kPathBlock, lds, s>>>(a);
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "paths_kernel launch");
+#ifdef LRT_EXP_STAMPS
+    {
+        unsigned long long h[3 * (kSecCount + 1)];
+        (void)hipMemcpyAsync(h, d_stamps, sizeof(h), hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        const char* names[] = {"trace", "light", "spec", "camera", "sched"};
+        for (int i = 0; i <= kSecCount; ++i)
+            fprintf(stderr, "stamps %-8s cycles %14llu  execs %10llu  lanes/exec %6.2f  cyc/exec %8.1f\n", names[i],
+                    h[3 * i], h[3 * i + 1], h[3 * i + 1] ? (double)h[3 * i + 2] / h[3 * i + 1] : 0.0,
+                    h[3 * i + 1] ? (double)h[3 * i] / h[3 * i + 1] : 0.0);
+    }
+#endif
     if (overflow) {
         e = hipFreeAsync(overflow, s);
         if (e != hipSuccess) return hip_fail(e, "hipFreeAsync(path stack overflow)");
@@ -347,8 +387,15 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     a.maxDepth = d->max_depth;
     a.out = reinterpret_cast<float4*>(d_buf);
     a.rays = d_rays;
-    const bool lds = !(d->flags & LRT_F_SCENE_GLOBAL) && a.count <= kLdsSphereLimit;
-    if (!(d->flags & LRT_F_SIMPLE)) {
+    const bool lds = !(d->flags & LRT_F_SCENE_GLOBAL) &&
+                     sizeof(float4) * (kTraceLdsLevels * kBlock + 4 * (size_t)a.count + a.nlights / 4 + 1) <= 64 * 1024;
+    // Kernel policy (measured, profiles/r1_*): with few samples per call the per-lane
+    // path count is too small for phase scheduling to pay for itself and v0 (one pixel
+    // per lane, reference-shaped loop) is fastest; from 8 samples per call on, v2's
+    // phase-scheduled static-pixel mode wins (config 3: 4.36 vs 5.24 ms).
+    int kflags = d->flags & (LRT_F_SIMPLE | LRT_F_V1 | LRT_F_V2S | LRT_F_V2);
+    if (kflags == 0) kflags = d->frames >= 8 ? LRT_F_V2S : LRT_F_SIMPLE;
+    if (!(kflags & LRT_F_SIMPLE)) {
         PathArgs p;
         p.cam = a.cam;
         p.sph = a.sph;
@@ -375,7 +422,24 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
         // next to the stack with room for 2 blocks per CU; otherwise it is read from global
         const bool lds_scene = !(d->flags & LRT_F_SCENE_GLOBAL) &&
                                2 * paths_lds_bytes(kLdsLevels, true, a.count, a.nlights) <= 160 * 1024;
-        return lds_scene ? launch_paths<true>(p, s) : launch_paths<false>(p, s);
+        const bool ovf = p.maxDepth > kLdsLevels;
+        if (kflags & LRT_F_V2S) {
+            const int pix = (d->flags >> 8) & 0xF;   // pixels per lane: 1 (default), 2 or 4
+            if (pix == 2) {
+                if (lds_scene) return ovf ? launch_paths<true, true, true, 2>(p, s) : launch_paths<true, true, false, 2>(p, s);
+                return ovf ? launch_paths<false, true, true, 2>(p, s) : launch_paths<false, true, false, 2>(p, s);
+            }
+            if (pix == 4) {
+                if (lds_scene) return ovf ? launch_paths<true, true, true, 4>(p, s) : launch_paths<true, true, false, 4>(p, s);
+                return ovf ? launch_paths<false, true, true, 4>(p, s) : launch_paths<false, true, false, 4>(p, s);
+            }
+            if (lds_scene) return ovf ? launch_paths<true, true, true, 1>(p, s) : launch_paths<true, true, false, 1>(p, s);
+            return ovf ? launch_paths<false, true, true, 1>(p, s) : launch_paths<false, true, false, 1>(p, s);
+        }
+        if (kflags & LRT_F_V1) return lds_scene ? launch_paths<true, false, true>(p, s)
+                                                  : launch_paths<false, false, true>(p, s);
+        if (lds_scene) return ovf ? launch_paths<true, true, true>(p, s) : launch_paths<true, true, false>(p, s);
+        return ovf ? launch_paths<false, true, true>(p, s) : launch_paths<false, true, false>(p, s);
     }
     dim3 grid((d->x_count + kTileX - 1) / kTileX, (d->row_count + kTileY - 1) / kTileY);
     hipError_t e;

@@ -167,7 +167,22 @@ LRT_CONST uint64_t kExp2Tab[32] = {
     0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
     0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
 
-LRT_HD double powf_log2_inline(uint32_t ix) {
+// The three powf tables, by pointer so a kernel can stage them in LDS (a per-lane table
+// gather from global memory is a VMEM op; see lrt_paths2.h).
+struct PowTables {
+    const double* invc;     // kPowLog2InvC
+    const double* logc;     // kPowLog2LogC
+    const uint64_t* exp2;   // kExp2Tab
+};
+LRT_HD PowTables pow_tables() {
+    PowTables t;
+    t.invc = kPowLog2InvC;
+    t.logc = kPowLog2LogC;
+    t.exp2 = kExp2Tab;
+    return t;
+}
+
+LRT_HD double powf_log2_inline(uint32_t ix, const PowTables& T) {
     const double A0 = 0x1.27616c9496e0bp-2, A1 = -0x1.71969a075c67ap-2, A2 = 0x1.ec70a6ca7baddp-2,
                  A3 = -0x1.7154748bef6c8p-1, A4 = 0x1.71547652ab82bp+0;
     uint32_t tmp = ix - 0x3f330000u;
@@ -175,8 +190,8 @@ LRT_HD double powf_log2_inline(uint32_t ix) {
     uint32_t top = tmp & 0xff800000u;
     uint32_t iz = ix - top;
     int k = (int32_t)top >> 23;
-    double invc = kPowLog2InvC[i];
-    double logc = kPowLog2LogC[i];
+    double invc = T.invc[i];
+    double logc = T.logc[i];
     double z = (double)u2f(iz);
     double r = __builtin_fma(z, invc, -1.0);
     double y0 = logc + (double)k;
@@ -190,14 +205,14 @@ LRT_HD double powf_log2_inline(uint32_t ix) {
     return y;
 }
 
-LRT_HD float powf_exp2_inline(double xd, uint32_t sign_bias) {
+LRT_HD float powf_exp2_inline(double xd, uint32_t sign_bias, const PowTables& T) {
     const double C0 = 0x1.c6af84b912394p-5, C1 = 0x1.ebfce50fac4f3p-3, C2 = 0x1.62e42ff0c52d6p-1;
     const double kShift = 0x1.8p+47;   // 0x1.8p52 / 32
     double kd = xd + kShift;
     uint64_t ki = d2u(kd);
     kd -= kShift;
     double r = xd - kd;
-    uint64_t t = kExp2Tab[ki % 32];
+    uint64_t t = T.exp2[ki % 32];
     uint64_t ski = ki + sign_bias;
     t += ski << (52 - 5);
     double s = u2d(t);
@@ -223,7 +238,7 @@ LRT_HD bool zeroinfnan(uint32_t ix) { return 2u * ix - 1u >= 2u * 0x7f800000u - 
 // powf(x, y) exactly as glibc 2.35's __powf (powf.c), signalling-NaN subtleties aside.
 // The path calls it as powf(1 - cosine, 5) (maths.h:126) and the present step as
 // powf(x, 0.416666667f) (main.cpp:112).
-LRT_HD float powf(float x, float y) {
+LRT_HD float powf(float x, float y, const PowTables& T) {
     const uint32_t kSignBias = 1u << (5 + 11);
     uint32_t sign_bias = 0;
     uint32_t ix = f2u(x), iy = f2u(y);
@@ -253,7 +268,7 @@ LRT_HD float powf(float x, float y) {
             ix -= 23u << 23;
         }
     }
-    double logx = powf_log2_inline(ix);
+    double logx = powf_log2_inline(ix, T);
     double ylogx = (double)y * logx;
     if (((d2u(ylogx) >> 47) & 0xffff) >= (d2u(126.0) >> 47)) {
         if (ylogx > 0x1.fffffffd1d571p+6) {   // __math_oflowf
@@ -265,10 +280,12 @@ LRT_HD float powf(float x, float y) {
             return (sign_bias ? -o : o) * o;
         }
     }
-    return powf_exp2_inline(ylogx, sign_bias);
+    return powf_exp2_inline(ylogx, sign_bias, T);
 }
 
-LRT_HD float powf5(float x) { return powf(x, 5.0f); }
+LRT_HD float powf(float x, float y) { return powf(x, y, pow_tables()); }
+LRT_HD float powf5(float x, const PowTables& T) { return powf(x, 5.0f, T); }
+LRT_HD float powf5(float x) { return powf(x, 5.0f, pow_tables()); }
 
 }  // namespace libm
 }  // namespace lrt

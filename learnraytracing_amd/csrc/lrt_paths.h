@@ -48,6 +48,7 @@ struct PathArgs {
     unsigned long long* rays;
     unsigned int* queue;        // zeroed before every launch
     float4* overflow;           // stack levels >= kLdsLevels: [level - kLdsLevels][global thread]
+    unsigned long long* stamps; // diagnostic builds only (-DLRT_EXP_STAMPS): per-section cycles
 };
 
 // Closest hit over all spheres: HitWorld's loop (parallel.cpp:54-73) with HitSphere's
@@ -114,9 +115,13 @@ struct PathStack {
 
 // LDS carve-up of paths_kernel: [stack kLdsLevels x 256][spheres N][materials 3N][lights]
 // (kLdsScene; otherwise only the stack is in LDS and the scene is read from global).
-__host__ __device__ inline size_t paths_lds_bytes(int lds_levels, bool lds_scene, int count, int nlights) {
-    size_t b = sizeof(float4) * (size_t)lds_levels * kPathBlock;
-    if (lds_scene) b += sizeof(float4) * 4 * (size_t)count + sizeof(int) * (size_t)(nlights > 0 ? nlights : 1);
+constexpr int kPowTableBytes = 16 * 8 + 16 * 8 + 32 * 8;   // powf tables (lrt_libm.h), staged by v2
+
+__host__ __device__ inline size_t paths_lds_bytes(int lds_levels, bool lds_scene, int count, int nlights,
+                                                   int pix = 0) {
+    size_t b = sizeof(float4) * (size_t)lds_levels * kPathBlock + kPowTableBytes;
+    if (lds_scene) b += sizeof(float4) * (4 * (size_t)count + (size_t)(nlights + 3) / 4 + 1);
+    b += sizeof(float4) * (size_t)pix * kPathBlock;   // static-mode pixel slots (v2)
     return b;
 }
 
@@ -135,7 +140,7 @@ __global__ __launch_bounds__(kPathBlock) void paths_kernel(const PathArgs a) {
     const float4* mats = a.mats;
     const int* lights = a.lights;
     if (kLdsScene) {
-        float4* s_sph = smem + kLdsLevels * kPathBlock;
+        float4* s_sph = smem + kLdsLevels * kPathBlock + kPowTableBytes / 16;
         float4* s_mat = s_sph + a.count;
         int* s_lights = reinterpret_cast<int*>(s_mat + 3 * a.count);
         for (int i = tid; i < a.count; i += kPathBlock) s_sph[i] = a.sph[i];

@@ -50,11 +50,12 @@ LRT_DEV bool refract(F3 v, F3 n, float nint, F3& out) {                         
     }
     return false;
 }
-LRT_DEV float schlick(float cosine, float ri) {                                     // maths.h:122-127
+LRT_DEV float schlick(float cosine, float ri, const libm::PowTables& T) {          // maths.h:122-127
     float r0 = (1.0f - ri) / (1.0f + ri);
     r0 = r0 * r0;
-    return r0 + (1.0f - r0) * libm::powf5(1.0f - cosine);
+    return r0 + (1.0f - r0) * libm::powf5(1.0f - cosine, T);
 }
+LRT_DEV float schlick(float cosine, float ri) { return schlick(cosine, ri, libm::pow_tables()); }
 
 struct Ray {                                                                        // maths.h:130-145
     F3 orig, dir;
@@ -144,11 +145,13 @@ struct SceneView {
 // is the reference's; hit position and normal are computed once for the winner
 // (they are pure functions of (ray, t, sphere), so this is bit-identical to the
 // reference overwriting them on every closer hit).
-LRT_DEV bool HitWorld(const Ray& r, float tMin, float tMax, const SceneView& sc, Hit& outHit, int& outID) {
+LRT_DEV int ClosestHitSV(const Ray& r, float tMin, float tMax, const SceneView& sc, float& tOut) {
     float closestT = tMax;
     int id = -1;
+    float4 next = sc.sph[0];
     for (int i = 0; i < sc.count; ++i) {
-        float4 s = sc.sph[i];
+        const float4 s = next;
+        if (i + 1 < sc.count) next = sc.sph[i + 1];
         F3 rs = f3(s.x, s.y, s.z) - r.orig;
         float rsProj = dot(rs, r.dir);
         float ifHit = dot(rs, rs) - rsProj * rsProj - s.w;
@@ -167,6 +170,12 @@ LRT_DEV bool HitWorld(const Ray& r, float tMin, float tMax, const SceneView& sc,
             }
         }
     }
+    tOut = closestT;
+    return id;
+}
+LRT_DEV bool HitWorld(const Ray& r, float tMin, float tMax, const SceneView& sc, Hit& outHit, int& outID) {
+    float closestT;
+    const int id = ClosestHitSV(r, tMin, tMax, sc, closestT);
     if (id < 0) return false;
     float4 s = sc.sph[id];
     outHit.pos = point_at(r, closestT);
@@ -202,10 +211,9 @@ LRT_DEV bool Scatter(const Material& mat, int matId, const Ray& r_in, const Hit&
             float phi = 2.0f * kPI * eps2;
             F3 l = su * libm::cosf(phi) * sinA + sv * libm::sinf(phi) * sinA + sw * cosA;   // :116
             l = normalize_member(l);                                                      // :117
-            Hit lightHit;
-            int hitID = -1;
+            float tLight;
             ++inoutRayCount;                                                              // :122
-            if (HitWorld(make_ray(rec.pos, l), kMinT, kMaxT, sc, lightHit, hitID) && hitID == i) {
+            if (ClosestHitSV(make_ray(rec.pos, l), kMinT, kMaxT, sc, tLight) == i) {     // HitWorld && hitID == i
                 float omega = 2.0f * kPI * (1.0f - cosAMax);
                 F3 rdir = r_in.dir;
                 F3 nl = dot(rec.normal, rdir) < 0.0f ? rec.normal : -rec.normal;
@@ -255,9 +263,22 @@ LRT_DEV bool Scatter(const Material& mat, int matId, const Ray& r_in, const Hit&
 // stack of (matE + lightE, material id); the fold T = E + att * T from the leaf
 // outwards reproduces the recursion's rounding exactly. maxDepth scatter events at
 // most (the reference's depth < kMaxDepth test); MAXD >= maxDepth.
+// lstk: this lane's LDS stack (kTraceLdsLevels levels, stride lstride float4); levels
+// beyond it (only when MAXD > kTraceLdsLevels) use a private array.
+constexpr int kTraceLdsLevels = 8;
 template <int MAXD>
-LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const SceneView& sc) {
-    float4 stack[MAXD > 0 ? MAXD : 1];
+LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const SceneView& sc,
+                 float4* lstk, int lstride) {
+    constexpr int kPriv = MAXD > kTraceLdsLevels ? MAXD - kTraceLdsLevels : 1;
+    float4 pstack[kPriv];
+    auto put = [&](int lvl, float4 v) {
+        if (MAXD <= kTraceLdsLevels || lvl < kTraceLdsLevels) lstk[lvl * lstride] = v;
+        else pstack[lvl - kTraceLdsLevels] = v;
+    };
+    auto get = [&](int lvl) -> float4 {
+        if (MAXD <= kTraceLdsLevels || lvl < kTraceLdsLevels) return lstk[lvl * lstride];
+        return pstack[lvl - kTraceLdsLevels];
+    };
     int depth = 0;
     F3 leaf;
     for (;;) {
@@ -276,7 +297,7 @@ LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const S
         if (depth < maxDepth &&
             Scatter(mat, id, r, rec, attenuation, scattered, lightE, inoutRayCount, rng, sc)) {
             F3 e = matE + lightE;
-            stack[depth] = make_float4(e.x, e.y, e.z, __int_as_float(id));
+            put(depth, make_float4(e.x, e.y, e.z, __int_as_float(id)));
             ++depth;
             r = scattered;
             continue;
@@ -286,7 +307,7 @@ LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const S
     }
     F3 T = leaf;
     for (int d = depth - 1; d >= 0; --d) {
-        float4 s = stack[d];
+        float4 s = get(d);
         float4 b = sc.mats[3 * __float_as_int(s.w) + 2];
         T = f3(s.x, s.y, s.z) + f3(b.x, b.y, b.z) * T;
     }

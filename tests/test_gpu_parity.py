@@ -41,11 +41,11 @@ def test_golden_mode_p(gpu, manifest, images, name):
     assert rays == fx["rays"]
 
 
-@pytest.mark.parametrize("flags", [0, 1, 2, 3])
+@pytest.mark.parametrize("flags", [0, 1, 2, 3, 4, 5, 8, 9, 16, 17, 8 | 2 << 8, 8 | 4 << 8, 9 | 4 << 8])
 @pytest.mark.parametrize("name", ["p_160x90_s4_d8", "p_96x54_s1_d50"])
 def test_golden_kernel_variants(gpu, manifest, images, flags, name):
-    """Both kernels (v1 path-regeneration megakernel, v0 pixel-per-lane with
-    LRT_F_SIMPLE) with LDS-staged or global scene reads give the same bits."""
+    """Every kernel (v2 default, v1 with LRT_F_V1, v0 with LRT_F_SIMPLE), with
+    LDS-staged or global scene reads, gives the same bits."""
     fx = manifest["fixtures"][name]
     buf, rays = _render(gpu, fx["w"], fx["h"], fx["frames"], fx["max_depth"], flags=flags)
     _assert_bitwise(buf, images[name], f"{name} flags={flags}")

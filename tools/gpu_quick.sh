@@ -23,7 +23,7 @@ python3 - <<'PY'
 import csv, collections
 agg=collections.defaultdict(list)
 for r in csv.DictReader(open('gpurun_out/q/pmc_counter_collection.csv')):
-    if 'paths_kernel' in r['Kernel_Name'] or 'trace_kernel' in r['Kernel_Name']:
+    if 'paths' in r['Kernel_Name'] or 'trace_kernel' in r['Kernel_Name']:
         agg[r['Counter_Name']].append(float(r['Counter_Value']))
 a={c: sum(v)/len(v) for c,v in agg.items()}
 print({c: '%.4g'%v for c,v in a.items()})
