@@ -147,9 +147,13 @@ def main():
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local_rank)
+    torch.cuda.set_device(local_rank if os.environ.get("LRT_DIST_BACKEND", "nccl") == "nccl" else 0)
+    backend = os.environ.get("LRT_DIST_BACKEND", "nccl")   # nccl = RCCL; gloo only to rehearse on 1 GPU
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
     import learnraytracing_amd as lrt
     from learnraytracing_amd.dist import gather_to_root, max_shard_rows, shard_rows
     from learnraytracing_amd.renderer import unshard_tensor
@@ -165,7 +169,7 @@ def main():
     flags = (1 if args.scene_global else 0) | {"auto": 0, "v0": 2, "v1": 4, "v2": 16, "v2s": 8, "v2s2": 8 | 2 << 8, "v2s4": 8 | 4 << 8}[args.kernel]
     job = lrt.Job(width=W, height=H, frame0=0, frames=spp_total, max_depth=D, row_block=rb,
                   row_period=world, row_phase=rank, row_count=rows, flags=flags)
-    dev = torch.device("cuda", local_rank)
+    dev = torch.device("cuda", torch.cuda.current_device())
     bufs = [torch.zeros((max_rows, W, 4), dtype=torch.float32, device=dev) for _ in range(2)]
     rays = torch.zeros(1, dtype=torch.int64, device=dev)
     gathered = [torch.empty((world, max_rows, W, 4), dtype=torch.float32, device=dev) if rank == 0 and world > 1
@@ -222,7 +226,8 @@ def main():
     elapsed = t1 - t0
     kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / max(1, args.steps)
 
-    stats = torch.tensor([elapsed, float(rays.item()), kernel_ms], dtype=torch.float64, device=dev)
+    stats = torch.tensor([elapsed, float(rays.item()), kernel_ms], dtype=torch.float64,
+                         device=dev if backend == "nccl" else "cpu")
     if world > 1:
         t = stats[0:1].clone()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -49,6 +49,16 @@ def gather_to_root(local, max_rows: int, world: int, rank: int, gathered=None, g
         raise ValueError("shard buffers must be padded to max_rows rows")
     if world == 1:
         return local.unsqueeze(0), None
+    if local.is_cuda and dist.get_backend(group) == "gloo":
+        # gloo gathers host tensors only (used to rehearse N>1 on one GPU / on CPU)
+        host = local.cpu()
+        hout = list(torch.empty((world,) + tuple(local.shape), dtype=local.dtype).unbind(0)) if rank == 0 else None
+        dist.gather(host, gather_list=hout, dst=0, group=group)
+        if rank == 0:
+            if gathered is None:
+                gathered = torch.empty((world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
+            gathered.copy_(torch.stack(hout))
+        return gathered, None
     out: Optional[List] = None
     if rank == 0:
         if gathered is None:
