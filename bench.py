@@ -121,7 +121,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=None, help="seconds of CPU-baseline timing")
     ap.add_argument("--scene-global", action="store_true", help="read spheres from global memory, not LDS")
-    ap.add_argument("--kernel", choices=["auto", "v0", "v1", "v2", "v2s", "v2s2", "v2s4"], default="auto",
+    ap.add_argument("--kernel", choices=["auto", "v0", "v1", "v2", "v2s"], default="auto",
                     help="auto: the library's policy (default); v0: one pixel per lane (LRT_F_SIMPLE); "
                          "v1: unscheduled state machine; v2: phase-scheduled persistent; v2s[N]: "
                          "phase-scheduled, N static pixels per lane")
@@ -166,7 +166,7 @@ def main():
     rb = H if world == 1 else args.row_block
     max_rows = max_shard_rows(H, rb, world)
     rows = shard_rows(H, rb, world, rank)
-    flags = (1 if args.scene_global else 0) | {"auto": 0, "v0": 2, "v1": 4, "v2": 16, "v2s": 8, "v2s2": 8 | 2 << 8, "v2s4": 8 | 4 << 8}[args.kernel]
+    flags = (1 if args.scene_global else 0) | {"auto": 0, "v0": 2, "v1": 4, "v2": 16, "v2s": 8}[args.kernel]
     job = lrt.Job(width=W, height=H, frame0=0, frames=spp_total, max_depth=D, row_block=rb,
                   row_period=world, row_phase=rank, row_count=rows, flags=flags)
     dev = torch.device("cuda", torch.cuda.current_device())

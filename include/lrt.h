@@ -99,10 +99,10 @@ typedef struct lrt_render_desc {
                                 (reference-shaped, for A/B and cross-checking)         */
 #define LRT_F_V1 4           /* v1 kernel: per-lane state machine without phase
                                 scheduling (for A/B); default is v2                    */
-#define LRT_F_V2S 8          /* v2 phase scheduling with static pixels per lane for the
-                                whole launch (no work queue); pixels per lane in bits
-                                8-11: LRT_F_PIX(1|2|4), default 1                      */
-#define LRT_F_PIX(n) ((n) << 8)
+#define LRT_F_V2S 8          /* v2 phase scheduling with one static pixel per lane for
+                                the whole launch (no work queue)                       */
+#define LRT_F_NO_BVH 32      /* scan every sphere (the reference's HitWorld loop) even
+                                when the scene has a BVH (> 16 spheres)                */
 #define LRT_F_V2 16          /* v2 persistent mode (work queue: static chunks, then
                                 atomics). With none of SIMPLE/V1/V2S/V2 set the library
                                 picks: SIMPLE below 8 frames per call, V2S from 8 on.  */
@@ -172,6 +172,12 @@ int lrt_present_bgra8(const float* d_rgba, uint32_t* d_bgra, int width, int heig
 int lrt_libm_eval_host(int kind, const float* in, float* out, long long n);
 /* Device evaluation of the same restatement (device pointers, blocking). */
 int lrt_libm_eval_device(int kind, const float* d_in, float* d_out, long long n);
+
+/* BVH diagnostics (host only, no GPU): build the BVH of the given scene and trace n rays
+ * (6 floats each: origin, direction) with the device traversal code. out[5]: mean nodes
+ * visited, mean spheres tested, max nodes, max spheres, fraction of rays whose closest
+ * hit differs from the linear scan (0 by construction). */
+int lrt_bvh_stats(const lrt_sphere* spheres, int count, const float* rays, int n, double* out);
 
 #ifdef __cplusplus
 }

@@ -29,6 +29,7 @@ F_SIMPLE = 2
 F_V1 = 4
 F_V2S = 8
 F_V2 = 16
+F_NO_BVH = 32
 
 
 class LrtError(RuntimeError):
@@ -98,6 +99,7 @@ SIGNATURES = {
     "lrt_present_bgra8": (_i, [_vp, _vp, _i, _i, _vp]),
     "lrt_libm_eval_host": (_i, [_i, _vp, _vp, _c.c_longlong]),
     "lrt_libm_eval_device": (_i, [_i, _vp, _vp, _c.c_longlong]),
+    "lrt_bvh_stats": (_i, [_c.POINTER(Sphere), _i, _vp, _i, _vp]),
 }
 
 _lock = threading.Lock()

@@ -1,0 +1,124 @@
+// Bit-exact BVH closest hit for N-sphere scenes (BASELINE configs 4-5).
+//
+// The reference scans every sphere in index order with a shrinking closestT
+// (HitWorld, parallel.cpp:54-73; HitSphere, maths.cpp:51-94). For sphere i define
+//     cand_i = t1 if t1 > tMin, else t2 if t2 > tMin, else +inf
+// with t1 = proj - halfCut, t2 = proj + halfCut computed exactly as HitSphere does.
+// cand_i does not depend on closestT, and sphere i replaces the running hit iff
+// cand_i < closestT (strict). Hence the scan returns the lexicographic minimum of
+// (cand_i, i) among spheres with cand_i < kMaxT: the smallest candidate, lowest index
+// on ties. Any traversal order that evaluates the same per-sphere arithmetic and
+// keeps (cand, index)-minimum returns the same id and t bit for bit, provided box
+// culling never drops a sphere that could win. Boxes are padded and the cull test
+// carries an absolute + relative margin far above float rounding (both set at build
+// time from the scene's extent), so culling is conservative.
+//
+// Layout (global memory, L1/L2 resident): BVH2 nodes of 4 float4 holding both
+// children's boxes. Child c: min.xyz + ref (int bits), max.xyz + count (int bits);
+// count > 0: leaf of `count` spheres starting at `ref` in the leaf-ordered sphere
+// array; count == 0: internal node `ref`; count < 0: empty. Leaf spheres are copies of
+// the scene's float4(center, r^2) plus the original index (materials, ties, lights all
+// keep using the original index).
+//
+// Included by lrt_trace.h (it uses F3, dot, kMinT, kMaxT defined there).
+#pragma once
+
+namespace lrt {
+
+constexpr int kBvhStackLevels = 24;   // builder guarantees depth <= 22
+
+struct BvhView {
+    const float4* nodes;    // 4 float4 per node, node 0 = root (none if nnodes == 0)
+    const float4* lsph;     // leaf-ordered spheres, then the `big` spheres
+    const int* lid;         // original index of each of those spheres
+    float margin;           // absolute cull margin (scene-extent scaled)
+    int on;                 // 0: linear scan
+    int nnodes;
+    int big0, nbig;         // spheres [big0, big0 + nbig) of lsph are tested before traversal:
+                            // spheres far larger than the rest (the ground, r = 100) would make
+                            // every ancestor box span the scene
+};
+
+LRT_DEV void SlabTest(const float4& mn, const float4& mx, const F3& o, const F3& inv, float& tn, float& tf) {
+    const float tx0 = (mn.x - o.x) * inv.x, tx1 = (mx.x - o.x) * inv.x;
+    const float ty0 = (mn.y - o.y) * inv.y, ty1 = (mx.y - o.y) * inv.y;
+    const float tz0 = (mn.z - o.z) * inv.z, tz1 = (mx.z - o.z) * inv.z;
+    // fminf/fmaxf drop a NaN operand (0 * inf on a slab plane): that axis then
+    // constrains nothing, which only ever keeps a node (conservative)
+    tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(tx0, tx1), __builtin_fminf(ty0, ty1)),
+                         __builtin_fminf(tz0, tz1));
+    tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(tx0, tx1), __builtin_fmaxf(ty0, ty1)),
+                         __builtin_fmaxf(tz0, tz1));
+}
+
+struct BvhStats { int nodes = 0, spheres = 0; };   // host diagnostics (lrt_bvh_stats)
+
+// stk: this lane's traversal stack (kBvhStackLevels entries, stride `stride`).
+LRT_DEV int ClosestHitBVH(const F3& o, const F3& d, const BvhView& bv, float& tOut, unsigned short* stk,
+                          int stride, BvhStats* st = nullptr) {
+    const F3 inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    float bestT = kMaxT;
+    int best = -1;
+    int sp = 0, cur = 0;
+    auto leaf = [&](int ref, int cnt) {
+        if (st) st->spheres += cnt;
+        for (int j = 0; j < cnt; ++j) {
+            const float4 s = bv.lsph[ref + j];
+            const F3 rs = f3(s.x, s.y, s.z) - o;                       // maths.cpp:54-59
+            const float rsProj = dot(rs, d);
+            const float ifHit = dot(rs, rs) - rsProj * rsProj - s.w;
+            if (ifHit < 0.0f) {
+                const float halfCut = __builtin_sqrtf(-ifHit);
+                const float t1 = rsProj - halfCut;
+                const float t2 = rsProj + halfCut;
+                const float cand = t1 > kMinT ? t1 : (t2 > kMinT ? t2 : __builtin_inff());
+                const int id = bv.lid[ref + j];
+                if (cand < bestT || (cand == bestT && best >= 0 && id < best)) {
+                    bestT = cand;
+                    best = id;
+                }
+            }
+        }
+    };
+    leaf(bv.big0, bv.nbig);   // seeds bestT, which then culls the traversal
+    if (bv.nnodes == 0) {
+        tOut = bestT;
+        return best;
+    }
+    for (;;) {
+        const float4 a0 = bv.nodes[4 * cur + 0], a1 = bv.nodes[4 * cur + 1];
+        const float4 b0 = bv.nodes[4 * cur + 2], b1 = bv.nodes[4 * cur + 3];
+        if (st) st->nodes += 1;
+        float tnA, tfA, tnB, tfB;
+        SlabTest(a0, a1, o, inv, tnA, tfA);
+        SlabTest(b0, b1, o, inv, tnB, tfB);
+        // conservative margins: absolute (scene extent) + relative to the distances compared
+        const float mb = bv.margin + 1e-5f * bestT;
+        const float mA = bv.margin + 1e-5f * __builtin_fabsf(tfA);
+        const float mB = bv.margin + 1e-5f * __builtin_fabsf(tfB);
+        const int cntA = lrt::libm::f2u_i(a1.w), cntB = lrt::libm::f2u_i(b1.w);
+        const bool hitA = cntA >= 0 && tnA <= tfA + mA && tnA <= bestT + mb && tfA >= kMinT - mA;
+        const bool hitB = cntB >= 0 && tnB <= tfB + mB && tnB <= bestT + mb && tfB >= kMinT - mB;
+        if (hitA && cntA > 0) leaf(lrt::libm::f2u_i(a0.w), cntA);
+        if (hitB && cntB > 0) leaf(lrt::libm::f2u_i(b0.w), cntB);
+        const bool goA = hitA && cntA == 0, goB = hitB && cntB == 0;
+        if (goA && goB) {
+            const bool aFirst = tnA <= tnB;
+            stk[sp * stride] = (unsigned short)lrt::libm::f2u_i(aFirst ? b0.w : a0.w);
+            ++sp;
+            cur = lrt::libm::f2u_i(aFirst ? a0.w : b0.w);
+        } else if (goA) {
+            cur = lrt::libm::f2u_i(a0.w);
+        } else if (goB) {
+            cur = lrt::libm::f2u_i(b0.w);
+        } else {
+            if (sp == 0) break;
+            --sp;
+            cur = stk[sp * stride];
+        }
+    }
+    tOut = bestT;
+    return best;
+}
+
+}  // namespace lrt

@@ -11,6 +11,9 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
+#include <type_traits>
+#include <cmath>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -41,6 +44,8 @@ struct KernelArgs {
     int frame0, frames, maxDepth;
     float4* out;
     unsigned long long* rays;
+    BvhView bv;
+    int bvh_stack_offset;   // bytes into dynamic LDS
 };
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
@@ -51,7 +56,7 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 #ifndef LRT_WAVES_PER_EU
 #define LRT_WAVES_PER_EU 1
 #endif
-template <int MAXD, bool kLds>
+template <int MAXD, bool kLds, bool kBvh>
 __global__ __launch_bounds__(kBlock, LRT_WAVES_PER_EU) void trace_kernel(const KernelArgs a) {
     // LDS: [recursion stack kTraceLdsLevels x kBlock][spheres][materials][lights]
     extern __shared__ float4 smem[];
@@ -71,6 +76,9 @@ __global__ __launch_bounds__(kBlock, LRT_WAVES_PER_EU) void trace_kernel(const K
     sc.lights = kLds ? s_lights : a.lights;
     sc.count = a.count;
     sc.nlights = a.nlights;
+    sc.bv = a.bv;
+    sc.bstk = reinterpret_cast<unsigned short*>(reinterpret_cast<char*>(smem) + a.bvh_stack_offset) + tid;
+    sc.bstride = kBlock;
 
     // 16x16 tile = 4 waves of 8x8 pixels
     const int wave = tid >> 6, lane = tid & 63;
@@ -90,7 +98,7 @@ __global__ __launch_bounds__(kBlock, LRT_WAVES_PER_EU) void trace_kernel(const K
             float u = ((float)x + RandomFloat01(rng)) * invWidth;              // :272
             float v = ((float)y + RandomFloat01(rng)) * invHeight;             // :273
             Ray r = GetRay(a.cam, u, v, rng);
-            F3 col = Trace<MAXD>(r, a.maxDepth, rays, rng, sc, smem + tid, kBlock);
+            F3 col = Trace<MAXD, kBvh>(r, a.maxDepth, rays, rng, sc, smem + tid, kBlock);
             F3 prev = f3(acc.x, acc.y, acc.z);
             col = prev * lerpFac + col * (1.0f - lerpFac);                     // :282
             acc.x = col.x;
@@ -160,6 +168,14 @@ struct Context {
     int* d_lights = nullptr;
     std::vector<lrt_sphere> spheres;
     std::vector<lrt_material> mats;
+    // BVH (scenes with more than kBvhMinSpheres spheres)
+    float4* d_bvh_nodes = nullptr;
+    float4* d_bvh_lsph = nullptr;
+    int* d_bvh_lid = nullptr;
+    float bvh_margin = 0.0f;
+    int bvh_nodes = 0;
+    int bvh_on = 0, bvh_big0 = 0, bvh_nbig = 0;
+
     float* d_frame = nullptr;   // lrt_draw_test / lrt_render_host staging
     size_t frame_bytes = 0;
     unsigned long long* d_rays = nullptr;
@@ -200,7 +216,143 @@ const lrt_material kDefaultMats[9] = {
     {LRT_LAMBERT, {0.8f, 0.6f, 0.2f}, {30, 25, 15}, 0, 0},
 };
 
+constexpr int kBvhMinSpheres = 16;
+constexpr int kBvhLeaf = 4;
+constexpr int kBvhMaxBuildDepth = 22;   // < kBvhStackLevels
+
+// ---- BVH build (host): median split on the longest centroid axis -------------------
+struct BvhPrim {
+    float lo[3], hi[3], c[3];
+    int id;
+};
+struct BvhBuilder {
+    std::vector<BvhPrim> P;
+    std::vector<float4> nodes, lsph;
+    std::vector<int> lid;
+    const std::vector<float4>* sph = nullptr;
+
+    static void bounds(const BvhPrim* p, int n, float lo[3], float hi[3]) {
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = INFINITY;
+            hi[k] = -INFINITY;
+        }
+        for (int i = 0; i < n; ++i)
+            for (int k = 0; k < 3; ++k) {
+                lo[k] = std::min(lo[k], p[i].lo[k]);
+                hi[k] = std::max(hi[k], p[i].hi[k]);
+            }
+    }
+    int node(int begin, int end, int depth) {
+        const int idx = (int)(nodes.size() / 4);
+        nodes.resize(nodes.size() + 4);
+        const int n = end - begin;
+        float cl[3] = {INFINITY, INFINITY, INFINITY}, ch[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int i = begin; i < end; ++i)
+            for (int k = 0; k < 3; ++k) {
+                cl[k] = std::min(cl[k], P[i].c[k]);
+                ch[k] = std::max(ch[k], P[i].c[k]);
+            }
+        int axis = 0;
+        for (int k = 1; k < 3; ++k)
+            if (ch[k] - cl[k] > ch[axis] - cl[axis]) axis = k;
+        const int mid = begin + n / 2;
+        std::nth_element(P.begin() + begin, P.begin() + mid, P.begin() + end, [axis](const BvhPrim& x, const BvhPrim& y) {
+            return x.c[axis] < y.c[axis] || (x.c[axis] == y.c[axis] && x.id < y.id);
+        });
+        float4 child[2][2];
+        const int rng[2][2] = {{begin, mid}, {mid, end}};
+        for (int h = 0; h < 2; ++h) {
+            const int b = rng[h][0], e = rng[h][1], cnt = e - b;
+            float lo[3], hi[3];
+            bounds(P.data() + b, cnt, lo, hi);
+            int ref, code;
+            if (cnt <= kBvhLeaf || depth + 1 >= kBvhMaxBuildDepth) {
+                ref = (int)lsph.size();
+                for (int i = b; i < e; ++i) {
+                    lsph.push_back((*sph)[P[i].id]);
+                    lid.push_back(P[i].id);
+                }
+                code = cnt;                      // leaf
+            } else {
+                ref = node(b, e, depth + 1);     // internal
+                code = 0;
+            }
+            float fr, fc;
+            memcpy(&fr, &ref, 4);
+            memcpy(&fc, &code, 4);
+            child[h][0] = make_float4(lo[0], lo[1], lo[2], fr);
+            child[h][1] = make_float4(hi[0], hi[1], hi[2], fc);
+        }
+        nodes[4 * idx + 0] = child[0][0];
+        nodes[4 * idx + 1] = child[0][1];
+        nodes[4 * idx + 2] = child[1][0];
+        nodes[4 * idx + 3] = child[1][1];
+        return idx;
+    }
+};
+
+struct BvhHost {
+    std::vector<float4> nodes, lsph;
+    std::vector<int> lid;
+    int big0 = 0, nbig = 0;
+    float margin = 0.0f;
+};
+
+// Spheres far larger than the typical one (the ground, r = 100) stay out of the tree and
+// are tested first; the rest get a BVH2 with leaves of <= kBvhLeaf spheres.
+void build_bvh_host(const lrt_sphere* s, int n, const std::vector<float4>& sph, BvhHost& out) {
+    std::vector<float> radii(n);
+    for (int i = 0; i < n; ++i) radii[i] = std::fabs(s[i].radius);
+    std::vector<float> sorted = radii;
+    std::nth_element(sorted.begin(), sorted.begin() + n / 2, sorted.end());
+    const float big_r = 8.0f * sorted[n / 2];
+    std::vector<int> big;
+    BvhBuilder B;
+    B.sph = &sph;
+    float extent = 1.0f;
+    for (int i = 0; i < n; ++i) {
+        if (radii[i] > big_r && big.size() < 16) {
+            big.push_back(i);
+            continue;
+        }
+        BvhPrim p;
+        const float r = radii[i];
+        const float c3[3] = {s[i].center.x, s[i].center.y, s[i].center.z};
+        for (int k = 0; k < 3; ++k) {
+            // conservative box: c +/- |r|, padded well beyond float rounding
+            const float pad = 1e-5f * (std::fabs(c3[k]) + r) + 1e-6f;
+            p.lo[k] = c3[k] - r - pad;
+            p.hi[k] = c3[k] + r + pad;
+            p.c[k] = c3[k];
+            extent = std::max(extent, std::max(std::fabs(p.lo[k]), std::fabs(p.hi[k])));
+        }
+        p.id = i;
+        B.P.push_back(p);
+    }
+    if (B.P.size() >= 2) B.node(0, (int)B.P.size(), 0);
+    else
+        for (const BvhPrim& p : B.P) big.push_back(p.id);
+    out.big0 = (int)B.lsph.size();
+    for (int i : big) {
+        B.lsph.push_back(sph[i]);
+        B.lid.push_back(i);
+    }
+    out.nbig = (int)big.size();
+    out.nodes.swap(B.nodes);
+    out.lsph.swap(B.lsph);
+    out.lid.swap(B.lid);
+    out.margin = 1e-5f * extent + 1e-4f;
+}
+
 void free_scene(Context& c) {
+    if (c.d_bvh_nodes) (void)hipFree(c.d_bvh_nodes);
+    if (c.d_bvh_lsph) (void)hipFree(c.d_bvh_lsph);
+    if (c.d_bvh_lid) (void)hipFree(c.d_bvh_lid);
+    c.d_bvh_nodes = nullptr;
+    c.d_bvh_lsph = nullptr;
+    c.d_bvh_lid = nullptr;
+    c.bvh_nodes = 0;
+    c.bvh_on = 0;
     if (c.d_sph) (void)hipFree(c.d_sph);
     if (c.d_mats) (void)hipFree(c.d_mats);
     if (c.d_lights) (void)hipFree(c.d_lights);
@@ -236,6 +388,22 @@ int upload_scene(Context& c, const lrt_sphere* s, const lrt_material* m, int n) 
     LRT_HIP(hipMemcpy(c.d_mats, mats.data(), sizeof(float4) * 3 * n, hipMemcpyHostToDevice));
     if (!lights.empty())
         LRT_HIP(hipMemcpy(c.d_lights, lights.data(), sizeof(int) * lights.size(), hipMemcpyHostToDevice));
+    if (n > kBvhMinSpheres) {
+        BvhHost B;
+        build_bvh_host(s, n, sph, B);
+        LRT_HIP(hipMalloc(&c.d_bvh_nodes, sizeof(float4) * std::max<size_t>(B.nodes.size(), 4)));
+        LRT_HIP(hipMalloc(&c.d_bvh_lsph, sizeof(float4) * B.lsph.size()));
+        LRT_HIP(hipMalloc(&c.d_bvh_lid, sizeof(int) * B.lid.size()));
+        if (!B.nodes.empty())
+            LRT_HIP(hipMemcpy(c.d_bvh_nodes, B.nodes.data(), sizeof(float4) * B.nodes.size(), hipMemcpyHostToDevice));
+        LRT_HIP(hipMemcpy(c.d_bvh_lsph, B.lsph.data(), sizeof(float4) * B.lsph.size(), hipMemcpyHostToDevice));
+        LRT_HIP(hipMemcpy(c.d_bvh_lid, B.lid.data(), sizeof(int) * B.lid.size(), hipMemcpyHostToDevice));
+        c.bvh_nodes = (int)(B.nodes.size() / 4);
+        c.bvh_big0 = B.big0;
+        c.bvh_nbig = B.nbig;
+        c.bvh_margin = B.margin;
+        c.bvh_on = 1;
+    }
     c.count = n;
     c.nlights = (int)lights.size();
     c.spheres.assign(s, s + n);
@@ -280,23 +448,32 @@ int validate(const lrt_render_desc* d) {
 }
 
 template <int MAXD>
-hipError_t launch_depth(const KernelArgs& a, bool lds, dim3 grid, hipStream_t s) {
+hipError_t launch_depth(KernelArgs a, bool lds, dim3 grid, hipStream_t s) {
     const size_t stack = sizeof(float4) * kTraceLdsLevels * kBlock;
-    if (lds) {
-        const size_t scene = sizeof(float4) * (4 * (size_t)a.count + (size_t)(a.nlights + 3) / 4 + 1);
-        trace_kernel<MAXD, true><<<grid, kBlock, stack + scene, s>>>(a);
+    const size_t scene = lds ? sizeof(float4) * (4 * (size_t)a.count + (size_t)(a.nlights + 3) / 4 + 1) : 0;
+    a.bvh_stack_offset = (int)(stack + scene);
+    const size_t bstk = a.bv.on ? sizeof(unsigned short) * kBvhStackLevels * kBlock : 0;
+    if (a.bv.on) {
+        if (lds)
+            trace_kernel<MAXD, true, true><<<grid, kBlock, stack + scene + bstk, s>>>(a);
+        else
+            trace_kernel<MAXD, false, true><<<grid, kBlock, stack + bstk, s>>>(a);
     } else {
-        trace_kernel<MAXD, false><<<grid, kBlock, stack, s>>>(a);
+        if (lds)
+            trace_kernel<MAXD, true, false><<<grid, kBlock, stack + scene, s>>>(a);
+        else
+            trace_kernel<MAXD, false, false><<<grid, kBlock, stack, s>>>(a);
     }
     return hipGetLastError();
 }
 
-template <bool kLdsScene, bool kV2, bool kOverflow, int kPix = 0>
+template <bool kLdsScene, bool kV2, bool kOverflow, int kPix = 0, bool kBvh = false>
 int launch_paths(PathArgs& a, hipStream_t s) {
     constexpr bool kStaticPixel = kPix > 0;
-    const size_t lds = paths_lds_bytes(kLdsLevels, kLdsScene, a.count, a.nlights, kPix);
+    const size_t lds = paths_lds_bytes(kLdsLevels, kLdsScene, a.count, a.nlights, kPix, a.bv.on != 0);
+    a.bvh_stack_offset = (int)paths_lds_bytes(kLdsLevels, kLdsScene, a.count, a.nlights, kPix, false);
     int per_cu = 0;
-    const void* kern = kV2 ? (const void*)paths2_kernel<kLdsLevels, kLdsScene, kOverflow, kPix>
+    const void* kern = kV2 ? (const void*)paths2_kernel<kLdsLevels, kLdsScene, kOverflow, kPix, kBvh>
                            : (const void*)paths_kernel<kLdsLevels, kLdsScene>;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kPathBlock, lds);
     if (e != hipSuccess) return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
@@ -305,11 +482,11 @@ int launch_paths(PathArgs& a, hipStream_t s) {
     long long blocks = (long long)per_cu * g_ctx.num_cus;
     if (blocks > want) blocks = want;
     dim3 grid((unsigned)blocks);
-    if (kStaticPixel) {   // one pixel per lane: 16x16 tiles, no persistence
+    if (kStaticPixel) {   // kPix pixels per lane: 16 x 16*kPix tiles, no persistence
         grid = dim3((unsigned)((a.xc + 15) / 16), (unsigned)((a.rows + 16 * kPix - 1) / (16 * kPix)));
         blocks = (long long)grid.x * grid.y;
     }
-    const size_t gthreads = (size_t)blocks * kPathBlock;
+    const size_t gthreads = (size_t)blocks * kPathBlock;   // = gridDim.x * gridDim.y * kPathBlock
     float4* overflow = nullptr;
     if (a.maxDepth > kLdsLevels) {
         e = hipMallocAsync((void**)&overflow, sizeof(float4) * gthreads * (size_t)(a.maxDepth - kLdsLevels), s);
@@ -328,7 +505,7 @@ int launch_paths(PathArgs& a, hipStream_t s) {
     e = hipMemsetAsync(q, 0, sizeof(unsigned int), s);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(queue)");
     if (kV2)
-        paths2_kernel<kLdsLevels, kLdsScene, kOverflow, kPix><<<grid, kPathBlock, lds, s>>>(a);
+        paths2_kernel<kLdsLevels, kLdsScene, kOverflow, kPix, kBvh><<<grid, kPathBlock, lds, s>>>(a);
     else
         paths_kernel<kLdsLevels, kLdsScene><<<dim3((unsigned)blocks), kPathBlock, lds, s>>>(a);
     e = hipGetLastError();
@@ -387,6 +564,15 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     a.maxDepth = d->max_depth;
     a.out = reinterpret_cast<float4*>(d_buf);
     a.rays = d_rays;
+    a.bv.nodes = g_ctx.d_bvh_nodes;
+    a.bv.lsph = g_ctx.d_bvh_lsph;
+    a.bv.lid = g_ctx.d_bvh_lid;
+    a.bv.margin = g_ctx.bvh_margin;
+    a.bv.on = (g_ctx.bvh_on && !(d->flags & LRT_F_NO_BVH)) ? 1 : 0;
+    a.bv.nnodes = g_ctx.bvh_nodes;
+    a.bv.big0 = g_ctx.bvh_big0;
+    a.bv.nbig = g_ctx.bvh_nbig;
+    a.bvh_stack_offset = 0;
     const bool lds = !(d->flags & LRT_F_SCENE_GLOBAL) &&
                      sizeof(float4) * (kTraceLdsLevels * kBlock + 4 * (size_t)a.count + a.nlights / 4 + 1) <= 64 * 1024;
     // Kernel policy (measured, profiles/r1_*): with few samples per call the per-lane
@@ -418,28 +604,29 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
         p.nitems = a.xc * a.rows;
         p.out = a.out;
         p.rays = a.rays;
+        p.bv = a.bv;
+        if (kflags & LRT_F_V1) p.bv.on = 0;   // v1 (A/B only) scans linearly
+        p.bvh_stack_offset = 0;
         // the whole scene (spheres, materials, lights) is staged in LDS when it fits
         // next to the stack with room for 2 blocks per CU; otherwise it is read from global
         const bool lds_scene = !(d->flags & LRT_F_SCENE_GLOBAL) &&
                                2 * paths_lds_bytes(kLdsLevels, true, a.count, a.nlights) <= 160 * 1024;
         const bool ovf = p.maxDepth > kLdsLevels;
-        if (kflags & LRT_F_V2S) {
-            const int pix = (d->flags >> 8) & 0xF;   // pixels per lane: 1 (default), 2 or 4
-            if (pix == 2) {
-                if (lds_scene) return ovf ? launch_paths<true, true, true, 2>(p, s) : launch_paths<true, true, false, 2>(p, s);
-                return ovf ? launch_paths<false, true, true, 2>(p, s) : launch_paths<false, true, false, 2>(p, s);
-            }
-            if (pix == 4) {
-                if (lds_scene) return ovf ? launch_paths<true, true, true, 4>(p, s) : launch_paths<true, true, false, 4>(p, s);
-                return ovf ? launch_paths<false, true, true, 4>(p, s) : launch_paths<false, true, false, 4>(p, s);
-            }
-            if (lds_scene) return ovf ? launch_paths<true, true, true, 1>(p, s) : launch_paths<true, true, false, 1>(p, s);
-            return ovf ? launch_paths<false, true, true, 1>(p, s) : launch_paths<false, true, false, 1>(p, s);
+        // v2 variants: scene in LDS or global x overflow stack x static pixels x BVH
+        const bool stat = (kflags & LRT_F_V2S) != 0;
+        const bool bvh = p.bv.on != 0;
+        auto go = [&](auto lds, auto ovf) -> int {
+            constexpr bool L = decltype(lds)::value, O = decltype(ovf)::value;
+            if (stat) return bvh ? launch_paths<L, true, O, 1, true>(p, s) : launch_paths<L, true, O, 1, false>(p, s);
+            return bvh ? launch_paths<L, true, O, 0, true>(p, s) : launch_paths<L, true, O, 0, false>(p, s);
+        };
+        using T = std::true_type;
+        using F = std::false_type;
+        if (!(kflags & LRT_F_V1)) {
+            if (lds_scene) return ovf ? go(T{}, T{}) : go(T{}, F{});
+            return ovf ? go(F{}, T{}) : go(F{}, F{});
         }
-        if (kflags & LRT_F_V1) return lds_scene ? launch_paths<true, false, true>(p, s)
-                                                  : launch_paths<false, false, true>(p, s);
-        if (lds_scene) return ovf ? launch_paths<true, true, true>(p, s) : launch_paths<true, true, false>(p, s);
-        return ovf ? launch_paths<false, true, true>(p, s) : launch_paths<false, true, false>(p, s);
+        return lds_scene ? launch_paths<true, false, true>(p, s) : launch_paths<false, false, true>(p, s);   // v1
     }
     dim3 grid((d->x_count + kTileX - 1) / kTileX, (d->row_count + kTileY - 1) / kTileY);
     hipError_t e;
@@ -641,6 +828,51 @@ int lrt_present_bgra8(const float* d_rgba, uint32_t* d_bgra, int width, int heig
     hipStream_t s = (hipStream_t)stream;
     present_kernel<<<(n + 255) / 256, 256, 0, s>>>(reinterpret_cast<const float4*>(d_rgba), d_bgra, n);
     LRT_HIP(hipGetLastError());
+    return LRT_OK;
+}
+
+// Diagnostic (host only, no GPU): build the BVH of the given scene and trace n rays
+// (o.xyz, d.xyz; d normalised as the Ray ctor does) with the device traversal code.
+// out[0..4]: mean nodes visited, mean spheres tested, max nodes, max spheres, fraction of
+// rays whose (id, t) differs from the linear scan (must be 0).
+int lrt_bvh_stats(const lrt_sphere* spheres, int count, const float* rays, int n, double* out) {
+    if (!spheres || count < 2 || !rays || !out || n < 1) return fail(LRT_E_INVALID, "invalid arguments");
+    std::vector<float4> sph(count);
+    for (int i = 0; i < count; ++i) {
+        const float r = spheres[i].radius;
+        sph[i] = make_float4(spheres[i].center.x, spheres[i].center.y, spheres[i].center.z, r * r);
+    }
+    BvhHost H;
+    build_bvh_host(spheres, count, sph, H);
+    BvhView bv;
+    bv.nodes = H.nodes.data();
+    bv.lsph = H.lsph.data();
+    bv.lid = H.lid.data();
+    bv.margin = H.margin;
+    bv.on = 1;
+    bv.nnodes = (int)(H.nodes.size() / 4);
+    bv.big0 = H.big0;
+    bv.nbig = H.nbig;
+    double sn = 0, ss = 0, mn = 0, ms = 0, bad = 0;
+    unsigned short stk[kBvhStackLevels];
+    for (int i = 0; i < n; ++i) {
+        const Ray r = make_ray(f3(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]),
+                               f3(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]));
+        BvhStats st;
+        float t1, t2;
+        const int a = ClosestHitBVH(r.orig, r.dir, bv, t1, stk, 1, &st);
+        const int b = ClosestHit(r.orig, r.dir, sph.data(), count, t2);
+        if (a != b || memcmp(&t1, &t2, 4) != 0) bad += 1;
+        sn += st.nodes;
+        ss += st.spheres;
+        mn = std::max(mn, (double)st.nodes);
+        ms = std::max(ms, (double)st.spheres);
+    }
+    out[0] = sn / n;
+    out[1] = ss / n;
+    out[2] = mn;
+    out[3] = ms;
+    out[4] = bad / n;
     return LRT_OK;
 }
 

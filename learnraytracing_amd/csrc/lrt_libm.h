@@ -45,6 +45,7 @@ LRT_HD uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
 LRT_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
 LRT_HD uint64_t d2u(double d) { return __builtin_bit_cast(uint64_t, d); }
 LRT_HD double u2d(uint64_t u) { return __builtin_bit_cast(double, u); }
+LRT_HD int f2u_i(float f) { return __builtin_bit_cast(int, f); }
 LRT_HD uint32_t abstop12(float x) { return (f2u(x) >> 20) & 0x7ff; }
 
 // __sincosf_table[0] and [1] in glibc's field order {c0, c1, s1, c2, s2, c3, s3, c4};

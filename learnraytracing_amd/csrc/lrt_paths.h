@@ -49,6 +49,8 @@ struct PathArgs {
     unsigned int* queue;        // zeroed before every launch
     float4* overflow;           // stack levels >= kLdsLevels: [level - kLdsLevels][global thread]
     unsigned long long* stamps; // diagnostic builds only (-DLRT_EXP_STAMPS): per-section cycles
+    BvhView bv;                 // bv.on: closest hit by BVH traversal (v2)
+    int bvh_stack_offset;       // byte offset of the BVH traversal stacks in dynamic LDS
 };
 
 // Closest hit over all spheres: HitWorld's loop (parallel.cpp:54-73) with HitSphere's
@@ -118,10 +120,11 @@ struct PathStack {
 constexpr int kPowTableBytes = 16 * 8 + 16 * 8 + 32 * 8;   // powf tables (lrt_libm.h), staged by v2
 
 __host__ __device__ inline size_t paths_lds_bytes(int lds_levels, bool lds_scene, int count, int nlights,
-                                                   int pix = 0) {
+                                                   int pix = 0, bool bvh = false) {
     size_t b = sizeof(float4) * (size_t)lds_levels * kPathBlock + kPowTableBytes;
     if (lds_scene) b += sizeof(float4) * (4 * (size_t)count + (size_t)(nlights + 3) / 4 + 1);
     b += sizeof(float4) * (size_t)pix * kPathBlock;   // static-mode pixel slots (v2)
+    if (bvh) b += sizeof(unsigned short) * (size_t)kBvhStackLevels * kPathBlock;   // last
     return b;
 }
 

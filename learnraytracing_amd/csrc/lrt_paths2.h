@@ -41,7 +41,7 @@ constexpr int kStaticPercent = 85;
 #ifndef LRT_WAVES_PER_EU
 #define LRT_WAVES_PER_EU 1
 #endif
-template <int kLdsLevels, bool kLdsScene, bool kOverflow, int kPix>
+template <int kLdsLevels, bool kLdsScene, bool kOverflow, int kPix, bool kBvh>
 __global__ __launch_bounds__(kPathBlock, LRT_WAVES_PER_EU) void paths2_kernel(const PathArgs a) {
     constexpr bool kStaticPixel = kPix > 0;
     extern __shared__ float4 smem[];
@@ -51,8 +51,9 @@ __global__ __launch_bounds__(kPathBlock, LRT_WAVES_PER_EU) void paths2_kernel(co
     stk.lds = smem;
     stk.overflow = a.overflow;
     stk.tid = tid;
-    stk.gtid = (size_t)blockIdx.x * kPathBlock + tid;
-    stk.gthreads = (size_t)gridDim.x * kPathBlock;
+    // linear block id: the static-pixel mode launches a 2-D grid
+    stk.gtid = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kPathBlock + tid;
+    stk.gthreads = (size_t)gridDim.x * gridDim.y * kPathBlock;
     // powf tables (Dielectric's schlick) live in LDS
     double* s_pow = reinterpret_cast<double*>(smem + kLdsLevels * kPathBlock);
     {
@@ -85,6 +86,7 @@ __global__ __launch_bounds__(kPathBlock, LRT_WAVES_PER_EU) void paths2_kernel(co
     const float invWidth = 1.0f / (float)a.width;     // parallel.cpp:260
     const float invHeight = 1.0f / (float)a.height;   // parallel.cpp:261
     const int fend = a.frame0 + a.frames;
+    unsigned short* bstk = reinterpret_cast<unsigned short*>(reinterpret_cast<char*>(smem) + a.bvh_stack_offset) + tid;
 
     auto push = [&](int level, F3 E, int id) {
         const float4 v = make_float4(E.x, E.y, E.z, __int_as_float(id));
@@ -165,7 +167,7 @@ __global__ __launch_bounds__(kPathBlock, LRT_WAVES_PER_EU) void paths2_kernel(co
         if (sec == kSecTrace) {
             // ---- TRACE: the ray query, then classification -----------------------------
             if (state == sTrace) {
-                id = ClosestHit(o, d, sph, a.count, t);
+                id = kBvh ? ClosestHitBVH(o, d, a.bv, t, bstk, kPathBlock) : ClosestHit(o, d, sph, a.count, t);
                 if (shadowRay) {
                     state = sShadow;
                 } else if (id < 0) {                                             // sky :221-226

@@ -133,19 +133,28 @@ LRT_DEV Material load_material(const float4* __restrict__ mats, int id) {
     return m;
 }
 
+}  // namespace lrt
+#include "lrt_bvh.h"
+namespace lrt {
+
 struct SceneView {
     const float4* sph;                 // LDS or global
     const float4* __restrict__ mats;   // global (per-lane gather, L1/L2 resident)
     const int* __restrict__ lights;    // emissive sphere ids in index order
     int count;
     int nlights;
+    BvhView bv;                        // bv.on: closest hit by BVH traversal
+    unsigned short* bstk;              // this lane's BVH traversal stack (LDS)
+    int bstride;
 };
 
 // HitWorld + HitSphere (parallel.cpp:54-73, maths.cpp:51-94). The per-sphere test
 // is the reference's; hit position and normal are computed once for the winner
 // (they are pure functions of (ray, t, sphere), so this is bit-identical to the
 // reference overwriting them on every closer hit).
+template <bool kBvh = false>
 LRT_DEV int ClosestHitSV(const Ray& r, float tMin, float tMax, const SceneView& sc, float& tOut) {
+    if (kBvh) return ClosestHitBVH(r.orig, r.dir, sc.bv, tOut, sc.bstk, sc.bstride);   // tMin/tMax = kMinT/kMaxT
     float closestT = tMax;
     int id = -1;
     float4 next = sc.sph[0];
@@ -173,9 +182,10 @@ LRT_DEV int ClosestHitSV(const Ray& r, float tMin, float tMax, const SceneView& 
     tOut = closestT;
     return id;
 }
+template <bool kBvh = false>
 LRT_DEV bool HitWorld(const Ray& r, float tMin, float tMax, const SceneView& sc, Hit& outHit, int& outID) {
     float closestT;
-    const int id = ClosestHitSV(r, tMin, tMax, sc, closestT);
+    const int id = ClosestHitSV<kBvh>(r, tMin, tMax, sc, closestT);
     if (id < 0) return false;
     float4 s = sc.sph[id];
     outHit.pos = point_at(r, closestT);
@@ -187,6 +197,7 @@ LRT_DEV bool HitWorld(const Ray& r, float tMin, float tMax, const SceneView& sc,
 
 // Scatter (parallel.cpp:78-196). The reference's `&mat == &smat` self test is the
 // comparison of table indices (matId). lightE accumulates in the same order.
+template <bool kBvh = false>
 LRT_DEV bool Scatter(const Material& mat, int matId, const Ray& r_in, const Hit& rec, F3& attenuation,
                      Ray& scattered, F3& outLightE, int& inoutRayCount, uint32_t& rng, const SceneView& sc) {
     outLightE = f3(0.0f, 0.0f, 0.0f);
@@ -213,7 +224,7 @@ LRT_DEV bool Scatter(const Material& mat, int matId, const Ray& r_in, const Hit&
             l = normalize_member(l);                                                      // :117
             float tLight;
             ++inoutRayCount;                                                              // :122
-            if (ClosestHitSV(make_ray(rec.pos, l), kMinT, kMaxT, sc, tLight) == i) {     // HitWorld && hitID == i
+            if (ClosestHitSV<kBvh>(make_ray(rec.pos, l), kMinT, kMaxT, sc, tLight) == i) {   // HitWorld && hitID == i
                 float omega = 2.0f * kPI * (1.0f - cosAMax);
                 F3 rdir = r_in.dir;
                 F3 nl = dot(rec.normal, rdir) < 0.0f ? rec.normal : -rec.normal;
@@ -266,7 +277,7 @@ LRT_DEV bool Scatter(const Material& mat, int matId, const Ray& r_in, const Hit&
 // lstk: this lane's LDS stack (kTraceLdsLevels levels, stride lstride float4); levels
 // beyond it (only when MAXD > kTraceLdsLevels) use a private array.
 constexpr int kTraceLdsLevels = 8;
-template <int MAXD>
+template <int MAXD, bool kBvh = false>
 LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const SceneView& sc,
                  float4* lstk, int lstride) {
     constexpr int kPriv = MAXD > kTraceLdsLevels ? MAXD - kTraceLdsLevels : 1;
@@ -285,7 +296,7 @@ LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const S
         Hit rec;
         int id = 0;
         ++inoutRayCount;
-        if (!HitWorld(r, kMinT, kMaxT, sc, rec, id)) {
+        if (!HitWorld<kBvh>(r, kMinT, kMaxT, sc, rec, id)) {
             float t = 0.5f * (r.dir.y + 1.0f);
             leaf = ((1.0f - t) * f3(1.0f, 1.0f, 1.0f) + t * f3(0.5f, 0.7f, 1.0f)) * 0.3f;
             break;
@@ -295,7 +306,7 @@ LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const S
         Ray scattered;
         F3 attenuation, lightE;
         if (depth < maxDepth &&
-            Scatter(mat, id, r, rec, attenuation, scattered, lightE, inoutRayCount, rng, sc)) {
+            Scatter<kBvh>(mat, id, r, rec, attenuation, scattered, lightE, inoutRayCount, rng, sc)) {
             F3 e = matE + lightE;
             put(depth, make_float4(e.x, e.y, e.z, __int_as_float(id)));
             ++depth;
