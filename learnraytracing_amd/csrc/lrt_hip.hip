@@ -27,9 +27,28 @@
 
 namespace lrt {
 
-constexpr int kTileX = 16;
-constexpr int kTileY = 16;
-constexpr int kBlock = kTileX * kTileY;  // 4 waves
+#ifndef LRT_V0_BLOCK
+#define LRT_V0_BLOCK 64
+#endif
+// v0 workgroup: one wave by default. A wave finished early in a multi-wave block keeps
+// its slot (and the block's LDS) until the slowest wave ends; with path lengths as
+// uneven as these, single-wave blocks keep ~1 more wave resident per SIMD.
+constexpr int kBlock = LRT_V0_BLOCK;
+static_assert(kBlock == 64 || kBlock == 256, "v0 block: 1 or 4 waves");
+constexpr int kBlockWavesX = kBlock == 256 ? 2 : 1;           // waves per block in x
+constexpr int kBlockWavesY = kBlock / 64 / kBlockWavesX;       // and in y
+constexpr int kTileX = 8 * kBlockWavesX;                       // pixels per block in x
+#ifndef LRT_V0_DYNAMIC
+#define LRT_V0_DYNAMIC 1
+#endif
+// Work counters: same-address device-scope atomics serialise at ~12 ns each (measured
+// ~80/us chip-wide), so v0's tile queue and ray count are split over kV0Queues
+// counters, each on its own 512-B line; block b serves queue b % kV0Queues, which owns
+// tiles q, q + kV0Queues, ...
+constexpr int kV0Queues = 16;
+constexpr int kCtrStride = 64;   // u64s between counters
+static_assert(!LRT_V0_DYNAMIC || kBlock == 64, "dynamic v0 tiles are fetched per wave: one wave per block");
+
 constexpr int kMaxDepthSupported = 64;
 
 struct KernelArgs {
@@ -46,6 +65,9 @@ struct KernelArgs {
     unsigned long long* rays;
     BvhView bv;
     int bvh_stack_offset;   // bytes into dynamic LDS
+    float4* ovf;            // recursion stack levels >= kTraceLdsLevels (null when maxDepth fits)
+    unsigned long long* wtrace;   // LRT_EXP_WAVETRACE builds only: per-wave start/end/ids
+    unsigned long long* tiles;    // this launch's counters: [q] tile queue, [kV0Queues + q] ray count
 };
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
@@ -56,9 +78,19 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 #ifndef LRT_WAVES_PER_EU
 #define LRT_WAVES_PER_EU 1
 #endif
-template <int MAXD, bool kLds, bool kBvh>
+// v0: the reference's per-pixel loop (parallel.cpp:255-289) with each pixel's frames
+// spread over kSplit adjacent lanes. Lane `sub` traces frames frame0 + sub, + sub +
+// kSplit, ...; after each round of kSplit frames every lane of the pixel gathers the
+// round's colours and applies the reference's running lerp (:262, :282) in frame order,
+// so the accumulated value is bit-identical to the serial loop. Splitting multiplies the
+// number of independent wave tasks by kSplit (config 2: 57,600 instead of 14,400 for
+// 1,024 SIMDs) and shortens them, which evens out the tail.
+// The grid is persistent (as many blocks as fit, grid-stride over tiles): short wave
+// tasks dispatched one per workgroup are limited by the workgroup dispatch rate
+// (~80 waves/us chip-wide measured), which left SIMDs at ~2 of 4 resident waves.
+template <int MAXD, bool kLds, bool kBvh, int kSplit>
 __global__ __launch_bounds__(kBlock, LRT_WAVES_PER_EU) void trace_kernel(const KernelArgs a) {
-    // LDS: [recursion stack kTraceLdsLevels x kBlock][spheres][materials][lights]
+    // LDS: [recursion stack kTraceLdsLevels x kBlock][spheres][materials][lights][bvh stack]
     extern __shared__ float4 smem[];
     const int tid = threadIdx.x;
     float4* s_sph = smem + kTraceLdsLevels * kBlock;
@@ -79,36 +111,109 @@ __global__ __launch_bounds__(kBlock, LRT_WAVES_PER_EU) void trace_kernel(const K
     sc.bv = a.bv;
     sc.bstk = reinterpret_cast<unsigned short*>(reinterpret_cast<char*>(smem) + a.bvh_stack_offset) + tid;
     sc.bstride = kBlock;
+#ifdef LRT_EXP_WAVETRACE
+    const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    const size_t gtid = (size_t)blockIdx.x * kBlock + tid;
+    const size_t gthreads = (size_t)gridDim.x * kBlock;
 
-    // 16x16 tile = 4 waves of 8x8 pixels
+    // wave = 8 x (8 / kSplit) pixels x kSplit frame lanes; block = kBlockWavesX x kBlockWavesY waves
     const int wave = tid >> 6, lane = tid & 63;
-    const int lx = blockIdx.x * kTileX + (wave & 1) * 8 + (lane & 7);
-    const int ly = blockIdx.y * kTileY + (wave >> 1) * 8 + (lane >> 3);
+    const int sub = lane % kSplit, p = lane / kSplit;
+    constexpr int kWaveRows = 8 / kSplit;
+    constexpr int kTileRows = kBlockWavesY * kWaveRows;
+    const int tilesX = (a.xc + kTileX - 1) / kTileX;
+    const int ntiles = tilesX * ((a.rows + kTileRows - 1) / kTileRows);
+    const float invWidth = 1.0f / (float)a.width;     // parallel.cpp:260
+    const float invHeight = 1.0f / (float)a.height;   // parallel.cpp:261
+    const int fend = a.frame0 + a.frames;
     int rays = 0;
-    if (lx < a.xc && ly < a.rows) {
+    const int q = blockIdx.x % kV0Queues;
+    const int bq = ((int)gridDim.x - q + kV0Queues - 1) / kV0Queues;   // blocks serving queue q
+    const int nq = (ntiles - q + kV0Queues - 1) / kV0Queues;            // tiles owned by queue q
+    unsigned long long* ctr = a.tiles + q * kCtrStride;
+    for (int i = blockIdx.x / kV0Queues; i < nq;) {
+        // Block b starts on its queue's tile b / kV0Queues; later tiles come from the
+        // queue's counter (zeroed by rays_collect_kernel after the launch). The fetch is
+        // issued here and consumed after the tile, so its latency hides behind the trace.
+        const int tile = q + kV0Queues * i;
+        unsigned long long fetched = 0;
+        if (LRT_V0_DYNAMIC && lane == 0) fetched = atomicAdd(ctr, 1ull);
+        const int lx = (tile % tilesX) * kTileX + (wave % kBlockWavesX) * 8 + (p & 7);
+        const int ly = (tile / tilesX) * kTileRows + (wave / kBlockWavesX) * kWaveRows + (p >> 3);
+        const bool valid = lx < a.xc && ly < a.rows;
         const int x = a.x0 + lx;
-        const int y = a.y0 + (ly / a.rb) * a.rb * a.rp + a.rph * a.rb + ly % a.rb;
-        const float invWidth = 1.0f / (float)a.width;     // parallel.cpp:260
-        const float invHeight = 1.0f / (float)a.height;   // parallel.cpp:261
+        const int y = valid ? a.y0 + (ly / a.rb) * a.rb * a.rp + a.rph * a.rb + ly % a.rb : 0;
         float4* px = a.out + (size_t)ly * a.xc + lx;
-        float4 acc = *px;
-        for (int f = a.frame0; f < a.frame0 + a.frames; ++f) {
-            uint32_t rng = PixelSeed((uint32_t)x, (uint32_t)y, (uint32_t)f);
-            const float lerpFac = (float)f / (float)(f + 1);                  // :262
-            float u = ((float)x + RandomFloat01(rng)) * invWidth;              // :272
-            float v = ((float)y + RandomFloat01(rng)) * invHeight;             // :273
-            Ray r = GetRay(a.cam, u, v, rng);
-            F3 col = Trace<MAXD, kBvh>(r, a.maxDepth, rays, rng, sc, smem + tid, kBlock);
-            F3 prev = f3(acc.x, acc.y, acc.z);
-            col = prev * lerpFac + col * (1.0f - lerpFac);                     // :282
-            acc.x = col.x;
-            acc.y = col.y;
-            acc.z = col.z;
+        float4 acc = valid ? *px : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        for (int f0 = a.frame0; f0 < fend; f0 += kSplit) {
+            const int f = f0 + sub;
+            F3 col = f3(0.0f, 0.0f, 0.0f);
+            if (valid && f < fend) {
+                uint32_t rng = PixelSeed((uint32_t)x, (uint32_t)y, (uint32_t)f);
+                float u = ((float)x + RandomFloat01(rng)) * invWidth;              // :272
+                float v = ((float)y + RandomFloat01(rng)) * invHeight;             // :273
+                Ray r = GetRay(a.cam, u, v, rng);
+                col = Trace<MAXD, kBvh>(r, a.maxDepth, rays, rng, sc, smem + tid, kBlock, a.ovf + gtid, gthreads);
+            }
+#pragma unroll
+            for (int j = 0; j < kSplit; ++j) {
+                const int src = lane - sub + j;
+                F3 c = kSplit == 1 ? col : f3(__shfl(col.x, src, 64), __shfl(col.y, src, 64), __shfl(col.z, src, 64));
+                const int fj = f0 + j;
+                if (fj < fend) {
+                    const float lerpFac = (float)fj / (float)(fj + 1);             // :262
+                    F3 prev = f3(acc.x, acc.y, acc.z);
+                    c = prev * lerpFac + c * (1.0f - lerpFac);                     // :282
+                    acc.x = c.x;
+                    acc.y = c.y;
+                    acc.z = c.z;
+                }
+            }
         }
-        *px = acc;
+        if (valid && sub == 0) *px = acc;
+        if (LRT_V0_DYNAMIC) {
+            const unsigned long long n = __shfl(fetched, 0, 64) + (unsigned long long)bq;
+            i = n < (unsigned long long)nq ? (int)n : nq;
+        } else {
+            i += bq;
+        }
     }
+    // one ray-count atomic per block: same-address atomics serialise in one L2 channel
+    __shared__ unsigned long long s_rays[kBlock / 64];
     unsigned long long total = wave_sum((unsigned long long)rays);
-    if (lane == 0 && total) atomicAdd(a.rays, total);
+    if (lane == 0) s_rays[wave] = total;
+    __syncthreads();
+#ifdef LRT_EXP_WAVETRACE
+    if (lane == 0) {
+        const size_t w = gtid >> 6;
+        a.wtrace[4 * w + 0] = wt0;
+        a.wtrace[4 * w + 1] = __builtin_amdgcn_s_memrealtime();
+        a.wtrace[4 * w + 2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);           // HW_ID
+        a.wtrace[4 * w + 3] = __builtin_amdgcn_s_getreg((15 << 11) | 20);          // XCC_ID
+    }
+#endif
+#ifndef LRT_EXP_NO_RAYCOUNT
+    if (tid == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < kBlock / 64; ++w) t += s_rays[w];
+        if (t) atomicAdd(a.tiles + (kV0Queues + q) * kCtrStride, t);
+    }
+#endif
+}
+
+// After a v0 launch (same stream): fold the per-queue ray counts into *rays and zero
+// the launch's counters for the slot's next use.
+__global__ void rays_collect_kernel(unsigned long long* tiles, unsigned long long* rays) {
+    const int l = threadIdx.x;
+    unsigned long long v = 0;
+    if (l < kV0Queues) {
+        v = tiles[(kV0Queues + l) * kCtrStride];
+        tiles[(kV0Queues + l) * kCtrStride] = 0;
+        tiles[l * kCtrStride] = 0;
+    }
+    v = wave_sum(v);
+    if (l == 0 && v) atomicAdd(rays, v);
 }
 
 // Frame assembly: shard g's local row ly -> global row (as lrt_render_desc's map).
@@ -153,6 +258,7 @@ __global__ void libm_kernel(int kind, const float* __restrict__ in, float* __res
 // ---------------------------------------------------------------------------------
 // host side
 constexpr int kQueueSlots = 64;
+constexpr size_t kTileSetU64 = 2 * kV0Queues * kCtrStride;   // one v0 launch's counters
 constexpr int kLdsLevels = 8;
 
 struct Context {
@@ -161,6 +267,8 @@ struct Context {
     int num_cus = 0;
     unsigned int* d_queue = nullptr;   // kQueueSlots work counters, one per in-flight launch
     unsigned queue_next = 0;
+    unsigned long long* d_tiles = nullptr;   // kQueueSlots x v0 counter sets (trace_kernel)
+    unsigned tiles_next = 0;
     hipStream_t stream = nullptr;
     int count = 0, nlights = 0;
     float4* d_sph = nullptr;
@@ -447,24 +555,120 @@ int validate(const lrt_render_desc* d) {
     return LRT_OK;
 }
 
-template <int MAXD>
-hipError_t launch_depth(KernelArgs a, bool lds, dim3 grid, hipStream_t s) {
+#ifdef LRT_EXP_WAVETRACE
+// Diagnostic build only: per-wave lifetimes of every v0 launch, appended to the binary
+// file $LRT_WAVETRACE (u64 nwaves, then nwaves x {t0, t1, hw_id, xcc_id}; t in 100 MHz ticks).
+unsigned long long* wavetrace_buffer(size_t waves) {
+    static unsigned long long* d = nullptr;
+    static size_t cap = 0;
+    if (waves > cap) {
+        if (d) (void)hipFree(d);
+        (void)hipMalloc(&d, sizeof(unsigned long long) * 4 * waves);
+        cap = waves;
+    }
+    return d;
+}
+void wavetrace_dump(unsigned long long* d, size_t waves, hipStream_t s) {
+    const char* path = getenv("LRT_WAVETRACE");
+    if (!path) return;
+    std::vector<unsigned long long> h(4 * waves);
+    (void)hipMemcpyAsync(h.data(), d, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost, s);
+    (void)hipStreamSynchronize(s);
+    FILE* f = fopen(path, "ab");
+    if (!f) return;
+    unsigned long long n = waves;
+    fwrite(&n, sizeof(n), 1, f);
+    fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
+    fclose(f);
+}
+#endif
+
+#ifndef LRT_V0_GRID_MULT
+#define LRT_V0_GRID_MULT 1
+#endif
+
+// Resident blocks per CU for (kernel, LDS bytes), cached: the query costs host time on
+// every launch otherwise.
+hipError_t occupancy(int* per_cu, const void* kern, int block, size_t lds) {
+    struct Entry { const void* k; int b; size_t l; int v; };
+    static Entry cache[32];
+    static int n = 0;
+    for (int i = 0; i < n; ++i)
+        if (cache[i].k == kern && cache[i].b == block && cache[i].l == lds) {
+            *per_cu = cache[i].v;
+            return hipSuccess;
+        }
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, kern, block, lds);
+    if (e == hipSuccess && n < 32) cache[n++] = {kern, block, lds, *per_cu};
+    return e;
+}
+
+#ifndef LRT_MAX_SPLIT
+#define LRT_MAX_SPLIT 4
+#endif
+
+template <int MAXD, int kSplit>
+int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
+    constexpr int kTileRows = kBlockWavesY * (8 / kSplit);
+    const long long ntiles = (long long)((xc + kTileX - 1) / kTileX) * ((rows + kTileRows - 1) / kTileRows);
     const size_t stack = sizeof(float4) * kTraceLdsLevels * kBlock;
     const size_t scene = lds ? sizeof(float4) * (4 * (size_t)a.count + (size_t)(a.nlights + 3) / 4 + 1) : 0;
     a.bvh_stack_offset = (int)(stack + scene);
     const size_t bstk = a.bv.on ? sizeof(unsigned short) * kBvhStackLevels * kBlock : 0;
+    const size_t ldsb = stack + (lds ? scene : 0) + bstk;
+    const void* kern = a.bv.on ? (lds ? (const void*)trace_kernel<MAXD, true, true, kSplit>
+                                      : (const void*)trace_kernel<MAXD, false, true, kSplit>)
+                               : (lds ? (const void*)trace_kernel<MAXD, true, false, kSplit>
+                                      : (const void*)trace_kernel<MAXD, false, false, kSplit>);
+    int per_cu = 0;
+    hipError_t e = occupancy(&per_cu, kern, kBlock, ldsb);
+    if (e != hipSuccess) return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
+    if (per_cu < 1) return fail(LRT_E_INVALID, "trace_kernel does not fit on a CU");
+    long long blocks = (long long)per_cu * g_ctx.num_cus * LRT_V0_GRID_MULT;
+    if (blocks > ntiles) blocks = ntiles;
+    const dim3 grid((unsigned)blocks);
+    a.ovf = nullptr;
+    a.tiles = g_ctx.d_tiles + (size_t)(g_ctx.tiles_next++ % kQueueSlots) * kTileSetU64;
+#ifdef LRT_EXP_WAVETRACE
+    a.wtrace = wavetrace_buffer((size_t)grid.x * (kBlock / 64));
+#endif
+    if (a.maxDepth > kTraceLdsLevels) {   // per resident thread: bounded by the persistent grid
+        const size_t gthreads = (size_t)grid.x * kBlock;
+        e = hipMallocAsync((void**)&a.ovf, sizeof(float4) * gthreads * (size_t)(a.maxDepth - kTraceLdsLevels), s);
+        if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(trace stack overflow)");
+    }
     if (a.bv.on) {
         if (lds)
-            trace_kernel<MAXD, true, true><<<grid, kBlock, stack + scene + bstk, s>>>(a);
+            trace_kernel<MAXD, true, true, kSplit><<<grid, kBlock, ldsb, s>>>(a);
         else
-            trace_kernel<MAXD, false, true><<<grid, kBlock, stack + bstk, s>>>(a);
+            trace_kernel<MAXD, false, true, kSplit><<<grid, kBlock, ldsb, s>>>(a);
     } else {
         if (lds)
-            trace_kernel<MAXD, true, false><<<grid, kBlock, stack + scene, s>>>(a);
+            trace_kernel<MAXD, true, false, kSplit><<<grid, kBlock, ldsb, s>>>(a);
         else
-            trace_kernel<MAXD, false, false><<<grid, kBlock, stack, s>>>(a);
+            trace_kernel<MAXD, false, false, kSplit><<<grid, kBlock, ldsb, s>>>(a);
     }
-    return hipGetLastError();
+    e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "trace_kernel launch");
+    rays_collect_kernel<<<1, 64, 0, s>>>(a.tiles, a.rays);
+    e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "rays_collect_kernel launch");
+#ifdef LRT_EXP_WAVETRACE
+    wavetrace_dump(a.wtrace, (size_t)grid.x * (kBlock / 64), s);
+#endif
+    if (a.ovf) {
+        e = hipFreeAsync(a.ovf, s);
+        if (e != hipSuccess) return hip_fail(e, "hipFreeAsync(trace stack overflow)");
+    }
+    return LRT_OK;
+}
+
+template <int MAXD>
+int launch_split(const KernelArgs& a, bool lds, int xc, int rows, int frames, hipStream_t s) {
+    // one lane per frame of a pixel, up to LRT_MAX_SPLIT lanes per pixel
+    if (LRT_MAX_SPLIT >= 4 && frames >= 4) return launch_depth<MAXD, (LRT_MAX_SPLIT >= 4 ? 4 : 1)>(a, lds, xc, rows, s);
+    if (LRT_MAX_SPLIT >= 2 && frames >= 2) return launch_depth<MAXD, (LRT_MAX_SPLIT >= 2 ? 2 : 1)>(a, lds, xc, rows, s);
+    return launch_depth<MAXD, 1>(a, lds, xc, rows, s);
 }
 
 template <bool kLdsScene, bool kV2, bool kOverflow, int kPix = 0, bool kBvh = false>
@@ -628,16 +832,9 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
         }
         return lds_scene ? launch_paths<true, false, true>(p, s) : launch_paths<false, false, true>(p, s);   // v1
     }
-    dim3 grid((d->x_count + kTileX - 1) / kTileX, (d->row_count + kTileY - 1) / kTileY);
-    hipError_t e;
-    if (d->max_depth <= 8)
-        e = launch_depth<8>(a, lds, grid, s);
-    else if (d->max_depth <= 20)
-        e = launch_depth<20>(a, lds, grid, s);
-    else
-        e = launch_depth<64>(a, lds, grid, s);
-    if (e != hipSuccess) return hip_fail(e, "trace_kernel launch");
-    return LRT_OK;
+    if (d->max_depth <= 8) return launch_split<8>(a, lds, d->x_count, d->row_count, d->frames, s);
+    if (d->max_depth <= 20) return launch_split<20>(a, lds, d->x_count, d->row_count, d->frames, s);
+    return launch_split<64>(a, lds, d->x_count, d->row_count, d->frames, s);
 }
 
 int ensure_frame(size_t bytes) {
@@ -717,7 +914,17 @@ int lrt_initialize(void) {
     LRT_HIP(hipStreamCreateWithFlags(&g_ctx.stream, hipStreamNonBlocking));
     LRT_HIP(hipMalloc(&g_ctx.d_rays, sizeof(unsigned long long)));
     LRT_HIP(hipMalloc(&g_ctx.d_queue, sizeof(unsigned int) * kQueueSlots));
+    LRT_HIP(hipMalloc(&g_ctx.d_tiles, sizeof(unsigned long long) * kQueueSlots * kTileSetU64));
+    LRT_HIP(hipMemset(g_ctx.d_tiles, 0, sizeof(unsigned long long) * kQueueSlots * kTileSetU64));
     LRT_HIP(hipDeviceGetAttribute(&g_ctx.num_cus, hipDeviceAttributeMultiprocessorCount, dev));
+    {   // keep freed stream-ordered blocks (the per-launch path-stack overflow) in the
+        // pool instead of returning them to the driver at every synchronisation
+        hipMemPool_t pool;
+        if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+            uint64_t keep = UINT64_MAX;
+            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+        }
+    }
     int rc = upload_scene(g_ctx, kDefaultSpheres, kDefaultMats, 9);
     if (rc) return rc;
     g_ctx.ready = true;
@@ -732,6 +939,8 @@ int lrt_shutdown(void) {
     if (g_ctx.d_frame) (void)hipFree(g_ctx.d_frame);
     if (g_ctx.d_rays) (void)hipFree(g_ctx.d_rays);
     if (g_ctx.d_queue) (void)hipFree(g_ctx.d_queue);
+    if (g_ctx.d_tiles) (void)hipFree(g_ctx.d_tiles);
+    g_ctx.d_tiles = nullptr;
     if (g_ctx.stream) (void)hipStreamDestroy(g_ctx.stream);
     g_ctx = Context();
     return LRT_OK;

@@ -274,21 +274,23 @@ LRT_DEV bool Scatter(const Material& mat, int matId, const Ray& r_in, const Hit&
 // stack of (matE + lightE, material id); the fold T = E + att * T from the leaf
 // outwards reproduces the recursion's rounding exactly. maxDepth scatter events at
 // most (the reference's depth < kMaxDepth test); MAXD >= maxDepth.
-// lstk: this lane's LDS stack (kTraceLdsLevels levels, stride lstride float4); levels
-// beyond it (only when MAXD > kTraceLdsLevels) use a private array.
-constexpr int kTraceLdsLevels = 8;
-template <int MAXD, bool kBvh = false>
+// lstk: this lane's LDS stack (kLdsLev levels, stride lstride float4); levels beyond
+// it (only when MAXD > kLdsLev) go to this lane's slice of a global overflow stack
+// (gstk, stride gstride; L2-resident -- few paths get that deep).
+#ifndef LRT_TRACE_LDS_LEVELS
+#define LRT_TRACE_LDS_LEVELS 8
+#endif
+constexpr int kTraceLdsLevels = LRT_TRACE_LDS_LEVELS;
+template <int MAXD, bool kBvh = false, int kLdsLev = kTraceLdsLevels>
 LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const SceneView& sc,
-                 float4* lstk, int lstride) {
-    constexpr int kPriv = MAXD > kTraceLdsLevels ? MAXD - kTraceLdsLevels : 1;
-    float4 pstack[kPriv];
+                 float4* lstk, int lstride, float4* gstk, size_t gstride) {
     auto put = [&](int lvl, float4 v) {
-        if (MAXD <= kTraceLdsLevels || lvl < kTraceLdsLevels) lstk[lvl * lstride] = v;
-        else pstack[lvl - kTraceLdsLevels] = v;
+        if (MAXD <= kLdsLev || lvl < kLdsLev) lstk[lvl * lstride] = v;
+        else gstk[(size_t)(lvl - kLdsLev) * gstride] = v;
     };
     auto get = [&](int lvl) -> float4 {
-        if (MAXD <= kTraceLdsLevels || lvl < kTraceLdsLevels) return lstk[lvl * lstride];
-        return pstack[lvl - kTraceLdsLevels];
+        if (MAXD <= kLdsLev || lvl < kLdsLev) return lstk[lvl * lstride];
+        return gstk[(size_t)(lvl - kLdsLev) * gstride];
     };
     int depth = 0;
     F3 leaf;

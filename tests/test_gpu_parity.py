@@ -247,3 +247,26 @@ def test_bvh_vs_oracle_random_scene(gpu):
     want, wrays = oracle.orc_render(640, 360, 3, 8, y0=150, yc=40, spheres=s, mats=m)
     _assert_bitwise(buf, want[..., :3], "bvh 300 spheres")
     assert rays == wrays
+
+
+def test_work_counters_across_slots_and_streams(gpu):
+    """v0's per-launch tile queues and ray counters live in rotating slots that the
+    launch's collect kernel zeroes: > 2 x 64 launches in a row, and launches in flight
+    on two streams at once, must all give the same image and ray count."""
+    import torch
+    want, wr = _render(gpu, 96, 54, 4, 8)
+    for _ in range(140):
+        got, r = _render(gpu, 96, 54, 4, 8)
+        assert r == wr
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    job = gpu.Job(width=320, height=180, frame0=0, frames=4, max_depth=8)
+    one, r1 = _render(gpu, 320, 180, 4, 8)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    bufs = [torch.zeros((180, 320, 4), dtype=torch.float32, device="cuda") for _ in range(8)]
+    rays = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(8)]
+    for i in range(8):
+        gpu.render_tensor(job, bufs[i], rays[i], streams[i % 2])
+    torch.cuda.synchronize()
+    for b, r in zip(bufs, rays):
+        assert int(r.item()) == r1
+        assert np.array_equal(b.cpu().numpy().view(np.uint32), one.view(np.uint32))
