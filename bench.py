@@ -94,7 +94,7 @@ def cpu_baseline(cfg, budget_s: float):
 
 def kernel_name(kernel: str, frames: int) -> str:
     if kernel == "auto":   # mirrors render_device's policy in lrt_hip.hip
-        kernel = "v2s" if frames >= 8 else "v0"
+        kernel = "v0"
     return {"v0": "trace_kernel", "v1": "paths_kernel"}.get(kernel, "paths2_kernel")
 
 

@@ -95,8 +95,9 @@ typedef struct lrt_render_desc {
 
 #define LRT_F_NONE 0
 #define LRT_F_SCENE_GLOBAL 1 /* read the scene from global memory instead of LDS staging */
-#define LRT_F_SIMPLE 2       /* v0 kernel: one work-item per pixel for all its samples
-                                (reference-shaped, for A/B and cross-checking)         */
+#define LRT_F_SIMPLE 2       /* v0 kernel (the default): the reference's per-pixel loop,
+                                a pixel's frames spread over adjacent lanes, persistent
+                                single-wave blocks fed from tile queues               */
 #define LRT_F_V1 4           /* v1 kernel: per-lane state machine without phase
                                 scheduling (for A/B); default is v2                    */
 #define LRT_F_V2S 8          /* v2 phase scheduling with one static pixel per lane for
@@ -105,7 +106,7 @@ typedef struct lrt_render_desc {
                                 when the scene has a BVH (> 16 spheres)                */
 #define LRT_F_V2 16          /* v2 persistent mode (work queue: static chunks, then
                                 atomics). With none of SIMPLE/V1/V2S/V2 set the library
-                                picks: SIMPLE below 8 frames per call, V2S from 8 on.  */
+                                runs SIMPLE (fastest on every measured config).        */
 
 /* ---- the reference API (parallel.h:6-8) ---------------------------------- */
 

@@ -75,8 +75,11 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
     return v;
 }
 
-#ifndef LRT_WAVES_PER_EU
-#define LRT_WAVES_PER_EU 1
+// 4 waves per SIMD: caps VGPRs at 128. The MAXD 20/64 and BVH instances otherwise
+// take 129-144 and drop to 3 waves (config 3: 4.44 -> 4.15 ms, config 4: 587 -> 538 ms
+// with the cap; the BVH instances spill 28-40 B/lane to scratch, which costs less).
+#ifndef LRT_V0_WAVES_PER_EU
+#define LRT_V0_WAVES_PER_EU 4
 #endif
 // v0: the reference's per-pixel loop (parallel.cpp:255-289) with each pixel's frames
 // spread over kSplit adjacent lanes. Lane `sub` traces frames frame0 + sub, + sub +
@@ -89,7 +92,7 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 // tasks dispatched one per workgroup are limited by the workgroup dispatch rate
 // (~80 waves/us chip-wide measured), which left SIMDs at ~2 of 4 resident waves.
 template <int MAXD, bool kLds, bool kBvh, int kSplit>
-__global__ __launch_bounds__(kBlock, LRT_WAVES_PER_EU) void trace_kernel(const KernelArgs a) {
+__global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(const KernelArgs a) {
     // LDS: [recursion stack kTraceLdsLevels x kBlock][spheres][materials][lights][bvh stack]
     extern __shared__ float4 smem[];
     const int tid = threadIdx.x;
@@ -779,12 +782,12 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     a.bvh_stack_offset = 0;
     const bool lds = !(d->flags & LRT_F_SCENE_GLOBAL) &&
                      sizeof(float4) * (kTraceLdsLevels * kBlock + 4 * (size_t)a.count + a.nlights / 4 + 1) <= 64 * 1024;
-    // Kernel policy (measured, profiles/r1_*): with few samples per call the per-lane
-    // path count is too small for phase scheduling to pay for itself and v0 (one pixel
-    // per lane, reference-shaped loop) is fastest; from 8 samples per call on, v2's
-    // phase-scheduled static-pixel mode wins (config 3: 4.36 vs 5.24 ms).
+    // Kernel policy (measured): v0 -- frames split over lanes, persistent single-wave
+    // blocks on spread tile queues, 4 waves/SIMD -- is fastest on every BASELINE config
+    // (config 2: 0.46 vs 0.64 ms, config 3: 4.15 vs 4.32 ms, config 4: 538 vs 575 ms
+    // for v2s); v1/v2/v2s stay selectable for A/B.
     int kflags = d->flags & (LRT_F_SIMPLE | LRT_F_V1 | LRT_F_V2S | LRT_F_V2);
-    if (kflags == 0) kflags = d->frames >= 8 ? LRT_F_V2S : LRT_F_SIMPLE;
+    if (kflags == 0) kflags = LRT_F_SIMPLE;
     if (!(kflags & LRT_F_SIMPLE)) {
         PathArgs p;
         p.cam = a.cam;
