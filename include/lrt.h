@@ -104,6 +104,12 @@ typedef struct lrt_render_desc {
                                 the whole launch (no work queue)                       */
 #define LRT_F_NO_BVH 32      /* scan every sphere (the reference's HitWorld loop) even
                                 when the scene has a BVH (> 16 spheres)                */
+#define LRT_F_NO_DOUBLE_LIGHT 64 /* opt-in GL-path rule (fragmentShader.fs.glsl:430,456-457,
+                                "doMaterialE"): a scatter event reached through a Lambert
+                                bounce does not add its emissive again (that light was
+                                sampled explicitly); the terminating hit always adds it.
+                                Off by default: the CPU reference double counts
+                                (parallel.cpp:214). v0 kernel only.                   */
 #define LRT_F_V2 16          /* v2 persistent mode (work queue: static chunks, then
                                 atomics). With none of SIMPLE/V1/V2S/V2 set the library
                                 runs SIMPLE (fastest on every measured config).        */
@@ -151,6 +157,33 @@ int lrt_render_device(const lrt_render_desc* desc, float* d_backbuffer,
 
 /* Same on a HOST buffer: H2D of prev, render, D2H, blocking. *out_rays = counted rays. */
 int lrt_render_host(const lrt_render_desc* desc, float* backbuffer, long long* out_rays);
+
+/* Opt-in first-hit features of the reference's GL path (fragmentShader.fs.glsl:444-451,
+ * 494-568): per pixel, running means (the backbuffer's lerp, parallel.cpp:282) of the
+ * first hit's normal, world position and material albedo (zero on a camera-ray miss),
+ * and running standard deviations (AdaptiveStdvar, :494-497, pow(x,2) taken as x*x) of
+ * the linear colour, the normal and the world position. Each non-NULL buffer has the
+ * backbuffer's shape (row_count * x_count RGBA float quads, alpha untouched) and is
+ * read and updated in place; features update for frames f <= max_frame (the GL path
+ * uses 4), every frame if max_frame < 0. The backbuffer is bit-identical to a render
+ * without features. v0 kernel only; a feature render keeps each pixel on one lane. */
+typedef struct lrt_features {
+    float* normal;
+    float* world_pos;
+    float* albedo;
+    float* color_std;
+    float* normal_std;
+    float* world_pos_std;
+    int32_t max_frame;
+    int32_t reserved;   /* 0 */
+} lrt_features;
+
+/* lrt_render_device / lrt_render_host with features (device resp. host buffers;
+ * features == NULL is the plain call). */
+int lrt_render_device_ex(const lrt_render_desc* desc, float* d_backbuffer,
+                         unsigned long long* d_rays, const lrt_features* d_features, void* stream);
+int lrt_render_host_ex(const lrt_render_desc* desc, float* backbuffer, long long* out_rays,
+                       const lrt_features* features);
 
 /* Number of local rows GPU `phase` owns in a row-block-cyclic split of `height` rows
  * into blocks of row_block rows dealt over `period` GPUs. */

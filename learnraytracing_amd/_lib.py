@@ -30,6 +30,7 @@ F_V1 = 4
 F_V2S = 8
 F_V2 = 16
 F_NO_BVH = 32
+F_NO_DOUBLE_LIGHT = 64
 
 
 class LrtError(RuntimeError):
@@ -77,6 +78,14 @@ class RenderDesc(ctypes.Structure):           # lrt_render_desc
                 ("max_depth", ctypes.c_int32), ("flags", ctypes.c_int32)]
 
 
+class Features(ctypes.Structure):             # lrt_features (fragmentShader.fs.glsl:444-451, 494-568)
+    _fields_ = [("normal", ctypes.c_void_p), ("world_pos", ctypes.c_void_p), ("albedo", ctypes.c_void_p),
+                ("color_std", ctypes.c_void_p), ("normal_std", ctypes.c_void_p),
+                ("world_pos_std", ctypes.c_void_p), ("max_frame", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+FEATURE_NAMES = ("normal", "world_pos", "albedo", "color_std", "normal_std", "world_pos_std")
+
 _c = ctypes
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
@@ -94,6 +103,8 @@ SIGNATURES = {
     "lrt_default_scene": (_i, [_c.POINTER(Sphere), _c.POINTER(Material), _i, _c.POINTER(_i)]),
     "lrt_render_device": (_i, [_c.POINTER(RenderDesc), _vp, _vp, _vp]),
     "lrt_render_host": (_i, [_c.POINTER(RenderDesc), _vp, _c.POINTER(_c.c_longlong)]),
+    "lrt_render_device_ex": (_i, [_c.POINTER(RenderDesc), _vp, _vp, _c.POINTER(Features), _vp]),
+    "lrt_render_host_ex": (_i, [_c.POINTER(RenderDesc), _vp, _c.POINTER(_c.c_longlong), _c.POINTER(Features)]),
     "lrt_shard_rows": (_i, [_i, _i, _i, _i]),
     "lrt_unshard_rows": (_i, [_vp, _vp, _i, _i, _i, _i, _vp]),
     "lrt_present_bgra8": (_i, [_vp, _vp, _i, _i, _vp]),

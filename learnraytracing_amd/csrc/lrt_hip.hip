@@ -68,7 +68,32 @@ struct KernelArgs {
     float4* ovf;            // recursion stack levels >= kTraceLdsLevels (null when maxDepth fits)
     unsigned long long* wtrace;   // LRT_EXP_WAVETRACE builds only: per-wave start/end/ids
     unsigned long long* tiles;    // this launch's counters: [q] tile queue, [kV0Queues + q] ray count
+    int ndl;                      // LRT_F_NO_DOUBLE_LIGHT
+    // lrt_features (kFeat launches): normal, world_pos, albedo, color_std, normal_std,
+    // world_pos_std (any may be null) and the last frame they are updated for (< 0: all)
+    float4* feat[6];
+    int featMax;
 };
+
+// AdaptiveStdvar (fragmentShader.fs.glsl:494-497) per channel, pow(x, 2) as x * x.
+LRT_DEV float adaptive_std(float lastStd, float lastMean, int n, float newVal, float newMean) {
+    const float nf = (float)n;
+    const float dm = lastMean - newMean, dv = newVal - newMean;
+    return __builtin_sqrtf((nf * (lastStd * lastStd) + nf * (dm * dm) + dv * dv) / (float)(n + 1));
+}
+LRT_DEV float4 adaptive_std3(float4 sd, float4 lastMean, F3 v, float4 newMean, int n) {
+    sd.x = adaptive_std(sd.x, lastMean.x, n, v.x, newMean.x);
+    sd.y = adaptive_std(sd.y, lastMean.y, n, v.y, newMean.y);
+    sd.z = adaptive_std(sd.z, lastMean.z, n, v.z, newMean.z);
+    return sd;
+}
+LRT_DEV float4 lerp_feature(float4 m, F3 v, float lerpFac) {   // parallel.cpp:282's lerp
+    F3 c = f3(m.x, m.y, m.z) * lerpFac + v * (1.0f - lerpFac);
+    m.x = c.x;
+    m.y = c.y;
+    m.z = c.z;
+    return m;
+}
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
@@ -91,8 +116,9 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 // The grid is persistent (as many blocks as fit, grid-stride over tiles): short wave
 // tasks dispatched one per workgroup are limited by the workgroup dispatch rate
 // (~80 waves/us chip-wide measured), which left SIMDs at ~2 of 4 resident waves.
-template <int MAXD, bool kLds, bool kBvh, int kSplit>
+template <int MAXD, bool kLds, bool kBvh, int kSplit, bool kFeat = false>
 __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(const KernelArgs a) {
+    static_assert(!kFeat || kSplit == 1, "feature launches keep a pixel's frames on one lane");
     // LDS: [recursion stack kTraceLdsLevels x kBlock][spheres][materials][lights][bvh stack]
     extern __shared__ float4 smem[];
     const int tid = threadIdx.x;
@@ -114,6 +140,9 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
     sc.bv = a.bv;
     sc.bstk = reinterpret_cast<unsigned short*>(reinterpret_cast<char*>(smem) + a.bvh_stack_offset) + tid;
     sc.bstride = kBlock;
+#ifdef LRT_EXP_SECSTATS
+    sc.secstats = a.wtrace;
+#endif
 #ifdef LRT_EXP_WAVETRACE
     const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -149,15 +178,25 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
         const int y = valid ? a.y0 + (ly / a.rb) * a.rb * a.rp + a.rph * a.rb + ly % a.rb : 0;
         float4* px = a.out + (size_t)ly * a.xc + lx;
         float4 acc = valid ? *px : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        float4 fb[6];   // feature running values (kFeat)
+        const size_t pix = (size_t)ly * a.xc + lx;
+        if constexpr (kFeat) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k)
+                fb[k] = (valid && a.feat[k]) ? a.feat[k][pix] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        }
         for (int f0 = a.frame0; f0 < fend; f0 += kSplit) {
             const int f = f0 + sub;
             F3 col = f3(0.0f, 0.0f, 0.0f);
+            F3 feat[3] = {f3(0.0f, 0.0f, 0.0f), f3(0.0f, 0.0f, 0.0f), f3(0.0f, 0.0f, 0.0f)};
             if (valid && f < fend) {
                 uint32_t rng = PixelSeed((uint32_t)x, (uint32_t)y, (uint32_t)f);
+                sec_count(sc, kSecCamera);
                 float u = ((float)x + RandomFloat01(rng)) * invWidth;              // :272
                 float v = ((float)y + RandomFloat01(rng)) * invHeight;             // :273
                 Ray r = GetRay(a.cam, u, v, rng);
-                col = Trace<MAXD, kBvh>(r, a.maxDepth, rays, rng, sc, smem + tid, kBlock, a.ovf + gtid, gthreads);
+                col = Trace<MAXD, kBvh, kFeat>(r, a.maxDepth, rays, rng, sc, smem + tid, kBlock, a.ovf + gtid,
+                                               gthreads, a.ndl, feat);
             }
 #pragma unroll
             for (int j = 0; j < kSplit; ++j) {
@@ -166,15 +205,33 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
                 const int fj = f0 + j;
                 if (fj < fend) {
                     const float lerpFac = (float)fj / (float)(fj + 1);             // :262
+                    const float4 last = acc;
                     F3 prev = f3(acc.x, acc.y, acc.z);
+                    const F3 sample = c;
                     c = prev * lerpFac + c * (1.0f - lerpFac);                     // :282
                     acc.x = c.x;
                     acc.y = c.y;
                     acc.z = c.z;
+                    if constexpr (kFeat) {   // fragmentShader.fs.glsl:536-568
+                        if (a.featMax < 0 || fj <= a.featMax) {
+                            fb[3] = adaptive_std3(fb[3], last, sample, acc, fj);
+                            const float4 lastN = fb[0], lastP = fb[1];
+                            fb[0] = lerp_feature(fb[0], feat[0], lerpFac);
+                            fb[1] = lerp_feature(fb[1], feat[1], lerpFac);
+                            fb[2] = lerp_feature(fb[2], feat[2], lerpFac);
+                            fb[4] = adaptive_std3(fb[4], lastN, feat[0], fb[0], fj);
+                            fb[5] = adaptive_std3(fb[5], lastP, feat[1], fb[1], fj);
+                        }
+                    }
                 }
             }
         }
         if (valid && sub == 0) *px = acc;
+        if constexpr (kFeat) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k)
+                if (valid && a.feat[k]) a.feat[k][pix] = fb[k];
+        }
         if (LRT_V0_DYNAMIC) {
             const unsigned long long n = __shfl(fetched, 0, 64) + (unsigned long long)bq;
             i = n < (unsigned long long)nq ? (int)n : nq;
@@ -288,6 +345,8 @@ struct Context {
     int bvh_on = 0, bvh_big0 = 0, bvh_nbig = 0;
 
     float* d_frame = nullptr;   // lrt_draw_test / lrt_render_host staging
+    float* d_feat[6] = {};      // lrt_render_host_ex feature staging
+    size_t feat_bytes[6] = {};
     size_t frame_bytes = 0;
     unsigned long long* d_rays = nullptr;
 };
@@ -610,7 +669,7 @@ hipError_t occupancy(int* per_cu, const void* kern, int block, size_t lds) {
 #define LRT_MAX_SPLIT 4
 #endif
 
-template <int MAXD, int kSplit>
+template <int MAXD, int kSplit, bool kFeat = false>
 int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     constexpr int kTileRows = kBlockWavesY * (8 / kSplit);
     const long long ntiles = (long long)((xc + kTileX - 1) / kTileX) * ((rows + kTileRows - 1) / kTileRows);
@@ -619,10 +678,10 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     a.bvh_stack_offset = (int)(stack + scene);
     const size_t bstk = a.bv.on ? sizeof(unsigned short) * kBvhStackLevels * kBlock : 0;
     const size_t ldsb = stack + (lds ? scene : 0) + bstk;
-    const void* kern = a.bv.on ? (lds ? (const void*)trace_kernel<MAXD, true, true, kSplit>
-                                      : (const void*)trace_kernel<MAXD, false, true, kSplit>)
-                               : (lds ? (const void*)trace_kernel<MAXD, true, false, kSplit>
-                                      : (const void*)trace_kernel<MAXD, false, false, kSplit>);
+    const void* kern = a.bv.on ? (lds ? (const void*)trace_kernel<MAXD, true, true, kSplit, kFeat>
+                                      : (const void*)trace_kernel<MAXD, false, true, kSplit, kFeat>)
+                               : (lds ? (const void*)trace_kernel<MAXD, true, false, kSplit, kFeat>
+                                      : (const void*)trace_kernel<MAXD, false, false, kSplit, kFeat>);
     int per_cu = 0;
     hipError_t e = occupancy(&per_cu, kern, kBlock, ldsb);
     if (e != hipSuccess) return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
@@ -632,6 +691,12 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     const dim3 grid((unsigned)blocks);
     a.ovf = nullptr;
     a.tiles = g_ctx.d_tiles + (size_t)(g_ctx.tiles_next++ % kQueueSlots) * kTileSetU64;
+#ifdef LRT_EXP_SECSTATS
+    static unsigned long long* d_sec = nullptr;
+    if (!d_sec) (void)hipMalloc(&d_sec, sizeof(unsigned long long) * 2 * kSecN * 16);
+    (void)hipMemsetAsync(d_sec, 0, sizeof(unsigned long long) * 2 * kSecN * 16, s);
+    a.wtrace = d_sec;
+#endif
 #ifdef LRT_EXP_WAVETRACE
     a.wtrace = wavetrace_buffer((size_t)grid.x * (kBlock / 64));
 #endif
@@ -642,14 +707,14 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     }
     if (a.bv.on) {
         if (lds)
-            trace_kernel<MAXD, true, true, kSplit><<<grid, kBlock, ldsb, s>>>(a);
+            trace_kernel<MAXD, true, true, kSplit, kFeat><<<grid, kBlock, ldsb, s>>>(a);
         else
-            trace_kernel<MAXD, false, true, kSplit><<<grid, kBlock, ldsb, s>>>(a);
+            trace_kernel<MAXD, false, true, kSplit, kFeat><<<grid, kBlock, ldsb, s>>>(a);
     } else {
         if (lds)
-            trace_kernel<MAXD, true, false, kSplit><<<grid, kBlock, ldsb, s>>>(a);
+            trace_kernel<MAXD, true, false, kSplit, kFeat><<<grid, kBlock, ldsb, s>>>(a);
         else
-            trace_kernel<MAXD, false, false, kSplit><<<grid, kBlock, ldsb, s>>>(a);
+            trace_kernel<MAXD, false, false, kSplit, kFeat><<<grid, kBlock, ldsb, s>>>(a);
     }
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "trace_kernel launch");
@@ -659,6 +724,23 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
 #ifdef LRT_EXP_WAVETRACE
     wavetrace_dump(a.wtrace, (size_t)grid.x * (kBlock / 64), s);
 #endif
+#ifdef LRT_EXP_SECSTATS
+    {
+        unsigned long long h[2 * kSecN * 16];
+        (void)hipMemcpyAsync(h, d_sec, sizeof(h), hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        const char* names[kSecN] = {"hit", "lambert", "shadow", "metal", "dielectric", "fold", "camera"};
+        for (int k = 0; k < kSecN; ++k) {
+            unsigned long long ex = 0, ln = 0;
+            for (int j = 0; j < 16; ++j) {
+                ex += h[2 * (k + kSecN * j)];
+                ln += h[2 * (k + kSecN * j) + 1];
+            }
+            fprintf(stderr, "secstats %-10s wave-execs %12llu  lanes %14llu  lanes/exec %6.2f\n", names[k], ex, ln,
+                    ex ? (double)ln / ex : 0.0);
+        }
+    }
+#endif
     if (a.ovf) {
         e = hipFreeAsync(a.ovf, s);
         if (e != hipSuccess) return hip_fail(e, "hipFreeAsync(trace stack overflow)");
@@ -667,7 +749,8 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
 }
 
 template <int MAXD>
-int launch_split(const KernelArgs& a, bool lds, int xc, int rows, int frames, hipStream_t s) {
+int launch_split(const KernelArgs& a, bool lds, int xc, int rows, int frames, bool feat, hipStream_t s) {
+    if (feat) return launch_depth<MAXD, 1, true>(a, lds, xc, rows, s);
     // one lane per frame of a pixel, up to LRT_MAX_SPLIT lanes per pixel
     if (LRT_MAX_SPLIT >= 4 && frames >= 4) return launch_depth<MAXD, (LRT_MAX_SPLIT >= 4 ? 4 : 1)>(a, lds, xc, rows, s);
     if (LRT_MAX_SPLIT >= 2 && frames >= 2) return launch_depth<MAXD, (LRT_MAX_SPLIT >= 2 ? 2 : 1)>(a, lds, xc, rows, s);
@@ -736,7 +819,8 @@ int launch_paths(PathArgs& a, hipStream_t s) {
     return LRT_OK;
 }
 
-int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_rays, hipStream_t s) {
+int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_rays, const lrt_features* feat,
+                  hipStream_t s) {
     int rc = validate(d);
     if (rc) return rc;
     if (!g_ctx.ready) return fail(LRT_E_STATE, "lrt_initialize() has not been called");
@@ -771,6 +855,18 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     a.maxDepth = d->max_depth;
     a.out = reinterpret_cast<float4*>(d_buf);
     a.rays = d_rays;
+    a.ndl = (d->flags & LRT_F_NO_DOUBLE_LIGHT) ? 1 : 0;
+    bool want_feat = false;
+    {
+        float* const fp[6] = {feat ? feat->normal : nullptr,    feat ? feat->world_pos : nullptr,
+                              feat ? feat->albedo : nullptr,    feat ? feat->color_std : nullptr,
+                              feat ? feat->normal_std : nullptr, feat ? feat->world_pos_std : nullptr};
+        for (int k = 0; k < 6; ++k) {
+            a.feat[k] = reinterpret_cast<float4*>(fp[k]);
+            want_feat = want_feat || fp[k] != nullptr;
+        }
+        a.featMax = feat ? feat->max_frame : -1;
+    }
     a.bv.nodes = g_ctx.d_bvh_nodes;
     a.bv.lsph = g_ctx.d_bvh_lsph;
     a.bv.lid = g_ctx.d_bvh_lid;
@@ -788,6 +884,8 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     // for v2s); v1/v2/v2s stay selectable for A/B.
     int kflags = d->flags & (LRT_F_SIMPLE | LRT_F_V1 | LRT_F_V2S | LRT_F_V2);
     if (kflags == 0) kflags = LRT_F_SIMPLE;
+    if ((a.ndl || want_feat) && !(kflags & LRT_F_SIMPLE))
+        return fail(LRT_E_INVALID, "LRT_F_NO_DOUBLE_LIGHT and features are implemented by the v0 kernel only");
     if (!(kflags & LRT_F_SIMPLE)) {
         PathArgs p;
         p.cam = a.cam;
@@ -835,9 +933,9 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
         }
         return lds_scene ? launch_paths<true, false, true>(p, s) : launch_paths<false, false, true>(p, s);   // v1
     }
-    if (d->max_depth <= 8) return launch_split<8>(a, lds, d->x_count, d->row_count, d->frames, s);
-    if (d->max_depth <= 20) return launch_split<20>(a, lds, d->x_count, d->row_count, d->frames, s);
-    return launch_split<64>(a, lds, d->x_count, d->row_count, d->frames, s);
+    if (d->max_depth <= 8) return launch_split<8>(a, lds, d->x_count, d->row_count, d->frames, want_feat, s);
+    if (d->max_depth <= 20) return launch_split<20>(a, lds, d->x_count, d->row_count, d->frames, want_feat, s);
+    return launch_split<64>(a, lds, d->x_count, d->row_count, d->frames, want_feat, s);
 }
 
 int ensure_frame(size_t bytes) {
@@ -850,7 +948,7 @@ int ensure_frame(size_t bytes) {
     return LRT_OK;
 }
 
-int render_host(const lrt_render_desc* d, float* buf, long long* out_rays) {
+int render_host(const lrt_render_desc* d, float* buf, long long* out_rays, const lrt_features* feat = nullptr) {
     int rc = validate(d);
     if (rc) return rc;
     if (!g_ctx.ready) return fail(LRT_E_STATE, "lrt_initialize() has not been called");
@@ -864,9 +962,34 @@ int render_host(const lrt_render_desc* d, float* buf, long long* out_rays) {
     hipStream_t s = g_ctx.stream;
     LRT_HIP(hipMemcpyAsync(g_ctx.d_frame, buf, bytes, hipMemcpyHostToDevice, s));
     LRT_HIP(hipMemsetAsync(g_ctx.d_rays, 0, sizeof(unsigned long long), s));
-    if ((rc = render_device(d, g_ctx.d_frame, g_ctx.d_rays, s))) return rc;
+    // host feature buffers go through device mirrors like the backbuffer
+    lrt_features dfeat;
+    memset(&dfeat, 0, sizeof(dfeat));
+    float* const hp[6] = {feat ? feat->normal : nullptr,    feat ? feat->world_pos : nullptr,
+                          feat ? feat->albedo : nullptr,    feat ? feat->color_std : nullptr,
+                          feat ? feat->normal_std : nullptr, feat ? feat->world_pos_std : nullptr};
+    float** const dp[6] = {&dfeat.normal, &dfeat.world_pos, &dfeat.albedo,
+                           &dfeat.color_std, &dfeat.normal_std, &dfeat.world_pos_std};
+    if (feat) {
+        dfeat.max_frame = feat->max_frame;
+        for (int k = 0; k < 6; ++k) {
+            if (!hp[k]) continue;
+            if (g_ctx.feat_bytes[k] < bytes) {
+                if (g_ctx.d_feat[k]) (void)hipFree(g_ctx.d_feat[k]);
+                g_ctx.d_feat[k] = nullptr;
+                g_ctx.feat_bytes[k] = 0;
+                if (hipMalloc(&g_ctx.d_feat[k], bytes) != hipSuccess) return fail(LRT_E_NOMEM, "hipMalloc(features)");
+                g_ctx.feat_bytes[k] = bytes;
+            }
+            *dp[k] = g_ctx.d_feat[k];
+            LRT_HIP(hipMemcpyAsync(g_ctx.d_feat[k], hp[k], bytes, hipMemcpyHostToDevice, s));
+        }
+    }
+    if ((rc = render_device(d, g_ctx.d_frame, g_ctx.d_rays, feat ? &dfeat : nullptr, s))) return rc;
     unsigned long long rays = 0;
     LRT_HIP(hipMemcpyAsync(buf, g_ctx.d_frame, bytes, hipMemcpyDeviceToHost, s));
+    for (int k = 0; k < 6; ++k)
+        if (hp[k]) LRT_HIP(hipMemcpyAsync(hp[k], g_ctx.d_feat[k], bytes, hipMemcpyDeviceToHost, s));
     LRT_HIP(hipMemcpyAsync(&rays, g_ctx.d_rays, sizeof(rays), hipMemcpyDeviceToHost, s));
     LRT_HIP(hipStreamSynchronize(s));
     if (out_rays) *out_rays = (long long)rays;
@@ -944,6 +1067,8 @@ int lrt_shutdown(void) {
     if (g_ctx.d_queue) (void)hipFree(g_ctx.d_queue);
     if (g_ctx.d_tiles) (void)hipFree(g_ctx.d_tiles);
     g_ctx.d_tiles = nullptr;
+    for (auto* f : g_ctx.d_feat)
+        if (f) (void)hipFree(f);
     if (g_ctx.stream) (void)hipStreamDestroy(g_ctx.stream);
     g_ctx = Context();
     return LRT_OK;
@@ -1001,7 +1126,19 @@ int lrt_default_scene(lrt_sphere* spheres, lrt_material* materials, int capacity
 
 int lrt_render_device(const lrt_render_desc* desc, float* d_backbuffer, unsigned long long* d_rays, void* stream) {
     std::lock_guard<std::mutex> lk(g_mu);
-    return render_device(desc, d_backbuffer, d_rays, (hipStream_t)stream);
+    return render_device(desc, d_backbuffer, d_rays, nullptr, (hipStream_t)stream);
+}
+
+int lrt_render_device_ex(const lrt_render_desc* desc, float* d_backbuffer, unsigned long long* d_rays,
+                         const lrt_features* d_features, void* stream) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    return render_device(desc, d_backbuffer, d_rays, d_features, (hipStream_t)stream);
+}
+
+int lrt_render_host_ex(const lrt_render_desc* desc, float* backbuffer, long long* out_rays,
+                       const lrt_features* features) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    return render_host(desc, backbuffer, out_rays, features);
 }
 
 int lrt_render_host(const lrt_render_desc* desc, float* backbuffer, long long* out_rays) {

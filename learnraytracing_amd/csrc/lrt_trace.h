@@ -146,7 +146,27 @@ struct SceneView {
     BvhView bv;                        // bv.on: closest hit by BVH traversal
     unsigned short* bstk;              // this lane's BVH traversal stack (LDS)
     int bstride;
+#ifdef LRT_EXP_SECSTATS
+    unsigned long long* secstats;      // diagnostic: per section {wave executions, active lanes}
+#endif
 };
+
+// Diagnostic builds only (LRT_EXP_SECSTATS): count how many lanes are active each time a
+// wave enters section `sec` (lane utilisation per section).
+enum { kSecHit, kSecLambert, kSecShadow, kSecMetal, kSecDiel, kSecFold, kSecCamera, kSecN };
+LRT_DEV void sec_count(const SceneView& sc, int sec) {
+#if defined(LRT_EXP_SECSTATS) && defined(__HIP_DEVICE_COMPILE__)
+    const unsigned long long m = __ballot(1);
+    if ((int)__lane_id() == __ffsll((long long)m) - 1) {
+        unsigned long long* g = sc.secstats + 2 * (sec + kSecN * (blockIdx.x & 15));
+        atomicAdd(g, 1ull);
+        atomicAdd(g + 1, (unsigned long long)__popcll(m));
+    }
+#else
+    (void)sc;
+    (void)sec;
+#endif
+}
 
 // HitWorld + HitSphere (parallel.cpp:54-73, maths.cpp:51-94). The per-sphere test
 // is the reference's; hit position and normal are computed once for the winner
@@ -185,6 +205,7 @@ LRT_DEV int ClosestHitSV(const Ray& r, float tMin, float tMax, const SceneView& 
 template <bool kBvh = false>
 LRT_DEV bool HitWorld(const Ray& r, float tMin, float tMax, const SceneView& sc, Hit& outHit, int& outID) {
     float closestT;
+    sec_count(sc, kSecHit);
     const int id = ClosestHitSV<kBvh>(r, tMin, tMax, sc, closestT);
     if (id < 0) return false;
     float4 s = sc.sph[id];
@@ -197,33 +218,45 @@ LRT_DEV bool HitWorld(const Ray& r, float tMin, float tMax, const SceneView& sc,
 
 // Scatter (parallel.cpp:78-196). The reference's `&mat == &smat` self test is the
 // comparison of table indices (matId). lightE accumulates in the same order.
+// Every material ends in `Ray(rec.pos, normalize(X))`, i.e. dir = normalize(normalize(X))
+// (the Ray ctor normalises again, maths.h:133-137), so ScatterDir returns X and the
+// caller forms the ray once for whichever materials the wave's lanes hold; Metal's
+// absorption test (:147) is applied there too. The attenuation is the material's
+// `att` row (albedo or 1), read back by the fold.
 template <bool kBvh = false>
-LRT_DEV bool Scatter(const Material& mat, int matId, const Ray& r_in, const Hit& rec, F3& attenuation,
-                     Ray& scattered, F3& outLightE, int& inoutRayCount, uint32_t& rng, const SceneView& sc) {
+LRT_DEV F3 ScatterDir(const Material& mat, int matId, const Ray& r_in, const Hit& rec, F3& outLightE,
+                      int& inoutRayCount, uint32_t& rng, const SceneView& sc) {
     outLightE = f3(0.0f, 0.0f, 0.0f);
     if (mat.type == 0) {  // Lambert :81-136
+        sec_count(sc, kSecLambert);
         F3 target = rec.pos + rec.normal + RandomUnitVector(rng);
-        scattered = make_ray(rec.pos, normalize(target - rec.pos));
-        attenuation = mat.albedo;
+        const F3 X = target - rec.pos;
         for (int k = 0; k < sc.nlights; ++k) {
             int i = sc.lights[k];
             if (i == matId) continue;  // :98
             float4 s = sc.sph[i];
             F3 c = f3(s.x, s.y, s.z);
-            F3 sw = normalize(c - rec.pos);
+            // sw = normalize(c - pos) and len = length(pos - c) (:103,:108): pos - c is
+            // -(c - pos) exactly, so both lengths are the same float -- computed once
+            const F3 cp = c - rec.pos;
+            const float len = length(cp);
+            const float kinv = 1.0f / len;
+            F3 sw = f3(cp.x * kinv, cp.y * kinv, cp.z * kinv);
             F3 su = normalize(cross(__builtin_fabsf(sw.x) > 0.01f ? f3(0.0f, 1.0f, 0.0f) : f3(1.0f, 0.0f, 0.0f), sw));
             F3 sv = cross(sw, su);
-            float len = length(rec.pos - c);
             float cosAMax = __builtin_sqrtf(1.0f - s.w / (len * len));                    // :109
             float eps1 = RandomFloat01(rng);
             float eps2 = RandomFloat01(rng);
             float cosA = 1.0f - eps1 + eps1 * cosAMax;
             float sinA = __builtin_sqrtf(1.0f - cosA * cosA);
             float phi = 2.0f * kPI * eps2;
-            F3 l = su * libm::cosf(phi) * sinA + sv * libm::sinf(phi) * sinA + sw * cosA;   // :116
+            float sphi, cphi;
+            libm::sincosf(phi, &sphi, &cphi);   // bit-identical to cosf(phi), sinf(phi)
+            F3 l = su * cphi * sinA + sv * sphi * sinA + sw * cosA;                         // :116
             l = normalize_member(l);                                                      // :117
             float tLight;
             ++inoutRayCount;                                                              // :122
+            sec_count(sc, kSecShadow);
             if (ClosestHitSV<kBvh>(make_ray(rec.pos, l), kMinT, kMaxT, sc, tLight) == i) {   // HitWorld && hitID == i
                 float omega = 2.0f * kPI * (1.0f - cosAMax);
                 F3 rdir = r_in.dir;
@@ -234,40 +267,35 @@ LRT_DEV bool Scatter(const Material& mat, int matId, const Ray& r_in, const Hit&
                 outLightE = outLightE + (mat.albedo * f3(e.x, e.y, e.z)) * (mx * omega / kPI);
             }
         }
-        return true;
+        return X;
     } else if (mat.type == 1) {  // Metal :137-148
+        sec_count(sc, kSecMetal);
         F3 refl = reflect(r_in.dir, rec.normal);
-        scattered = make_ray(rec.pos, normalize(refl + mat.roughness * RandomInUnitSphere(rng)));
-        attenuation = mat.albedo;
-        return dot(scattered.dir, rec.normal) > 0.0f;
-    } else if (mat.type == 2) {  // Dielectric :149-193
-        F3 outwardN;
-        F3 rdir = r_in.dir;
-        F3 refl = reflect(rdir, rec.normal);
-        float nint;
-        F3 refr = f3(0.0f, 0.0f, 0.0f);
-        float reflProb;
-        float cosine;
-        if (dot(rdir, rec.normal) > 0.0f) {
-            outwardN = -rec.normal;
-            nint = mat.ri;
-            cosine = dot(rdir, rec.normal);
-        } else {
-            outwardN = rec.normal;
-            nint = 1.0f / mat.ri;
-            cosine = -dot(rdir, rec.normal);
-        }
-        if (refract(rdir, outwardN, nint, refr))
-            reflProb = schlick(cosine, mat.ri);
-        else
-            reflProb = 1.0f;
-        if (RandomFloat01(rng) < reflProb)
-            scattered = make_ray(rec.pos, normalize(refl));
-        else
-            scattered = make_ray(rec.pos, normalize(refr));
-        attenuation = f3(1.0f, 1.0f, 1.0f);
+        return refl + mat.roughness * RandomInUnitSphere(rng);
     }
-    return true;
+    // Dielectric :149-193 (validate() admits types 0-2 only)
+    sec_count(sc, kSecDiel);
+    F3 outwardN;
+    F3 rdir = r_in.dir;
+    F3 refl = reflect(rdir, rec.normal);
+    float nint;
+    F3 refr = f3(0.0f, 0.0f, 0.0f);
+    float reflProb;
+    float cosine;
+    if (dot(rdir, rec.normal) > 0.0f) {
+        outwardN = -rec.normal;
+        nint = mat.ri;
+        cosine = dot(rdir, rec.normal);
+    } else {
+        outwardN = rec.normal;
+        nint = 1.0f / mat.ri;
+        cosine = -dot(rdir, rec.normal);
+    }
+    if (refract(rdir, outwardN, nint, refr))
+        reflProb = schlick(cosine, mat.ri);
+    else
+        reflProb = 1.0f;
+    return RandomFloat01(rng) < reflProb ? refl : refr;
 }
 
 // Trace (parallel.cpp:200-227) as a loop. Scatter events are pushed on a per-lane
@@ -281,9 +309,13 @@ LRT_DEV bool Scatter(const Material& mat, int matId, const Ray& r_in, const Hit&
 #define LRT_TRACE_LDS_LEVELS 8
 #endif
 constexpr int kTraceLdsLevels = LRT_TRACE_LDS_LEVELS;
-template <int MAXD, bool kBvh = false, int kLdsLev = kTraceLdsLevels>
+// ndl (LRT_F_NO_DOUBLE_LIGHT): the GL loop's doMaterialE rule (fragmentShader.fs.glsl:430,
+// 456-457) -- a scatter event reached through a Lambert bounce adds no emissive; the
+// terminating hit always does. kFeat: feat[0..2] receive the first hit's normal,
+// position and albedo (fragmentShader.fs.glsl:444-451; left untouched on a miss).
+template <int MAXD, bool kBvh = false, bool kFeat = false, int kLdsLev = kTraceLdsLevels>
 LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const SceneView& sc,
-                 float4* lstk, int lstride, float4* gstk, size_t gstride) {
+                 float4* lstk, int lstride, float4* gstk, size_t gstride, int ndl = 0, F3* feat = nullptr) {
     auto put = [&](int lvl, float4 v) {
         if (MAXD <= kLdsLev || lvl < kLdsLev) lstk[lvl * lstride] = v;
         else gstk[(size_t)(lvl - kLdsLev) * gstride] = v;
@@ -293,6 +325,7 @@ LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const S
         return gstk[(size_t)(lvl - kLdsLev) * gstride];
     };
     int depth = 0;
+    bool prevLambert = false;
     F3 leaf;
     for (;;) {
         Hit rec;
@@ -305,20 +338,31 @@ LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const S
         }
         Material mat = load_material(sc.mats, id);
         F3 matE = mat.emissive;
-        Ray scattered;
-        F3 attenuation, lightE;
-        if (depth < maxDepth &&
-            Scatter<kBvh>(mat, id, r, rec, attenuation, scattered, lightE, inoutRayCount, rng, sc)) {
-            F3 e = matE + lightE;
-            put(depth, make_float4(e.x, e.y, e.z, __int_as_float(id)));
-            ++depth;
-            r = scattered;
-            continue;
+        if (kFeat && depth == 0) {   // the first hit (depth 0 is only ever seen once)
+            feat[0] = rec.normal;
+            feat[1] = rec.pos;
+            feat[2] = mat.albedo;
+        }
+        if (depth < maxDepth) {   // :212
+            F3 lightE;
+            const F3 X = ScatterDir<kBvh>(mat, id, r, rec, lightE, inoutRayCount, rng, sc);
+            const F3 dir = normalize(normalize(X));
+            if (mat.type != 1 || dot(dir, rec.normal) > 0.0f) {   // Metal absorbs (:147)
+                if (ndl && prevLambert) matE = f3(0.0f, 0.0f, 0.0f);
+                prevLambert = mat.type == 0;
+                F3 e = matE + lightE;
+                put(depth, make_float4(e.x, e.y, e.z, __int_as_float(id)));
+                ++depth;
+                r.orig = rec.pos;
+                r.dir = dir;
+                continue;
+            }
         }
         leaf = matE;
         break;
     }
     F3 T = leaf;
+    sec_count(sc, kSecFold);
     for (int d = depth - 1; d >= 0; --d) {
         float4 s = get(d);
         float4 b = sc.mats[3 * __float_as_int(s.w) + 2];

@@ -119,6 +119,27 @@ def render_host(job: Job, backbuffer: np.ndarray) -> int:
     return rays.value
 
 
+def render_host_features(job: Job, backbuffer: np.ndarray, features: dict, max_frame: int = 4) -> int:
+    """render_host plus the GL path's first-hit features (lrt_render_host_ex): `features`
+    maps names of lrt_features ("normal", "world_pos", "albedo", "color_std", "normal_std",
+    "world_pos_std") to host float32 buffers shaped like the backbuffer, updated in place
+    for frames <= max_frame (< 0: all). Returns rays."""
+    d = job.desc()
+    n = d.row_count * d.x_count * 4
+    _check_host_buffer(backbuffer, n)
+    f = L.Features()
+    f.max_frame = int(max_frame)
+    for name, buf in features.items():
+        if name not in L.FEATURE_NAMES:
+            raise L.LrtError(L.LRT_E_INVALID, f"unknown feature {name!r}")
+        _check_host_buffer(buf, n)
+        setattr(f, name, buf.ctypes.data)
+    rays = ctypes.c_longlong(0)
+    L.check(L.lib().lrt_render_host_ex(ctypes.byref(d), backbuffer.ctypes.data_as(ctypes.c_void_p),
+                                       ctypes.byref(rays), ctypes.byref(f)))
+    return rays.value
+
+
 def render_device(job: Job, buf_ptr: int, rays_ptr: int, stream_ptr: int = 0) -> None:
     """Asynchronous render into device memory (raw pointers, e.g. torch's data_ptr())."""
     d = job.desc()

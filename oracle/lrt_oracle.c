@@ -133,7 +133,12 @@ typedef struct {
     const mat_t* mats;
     int count;
     int maxDepth;        /* scatter while depth < maxDepth (parallel.cpp:12,212) */
+    int noDoubleLight;   /* ORC_NO_DOUBLE_LIGHT: the GL path's doMaterialE rule */
 } scene_t;
+
+/* first-hit features of one sample (fragmentShader.fs.glsl:444-451: the first HitWorld
+ * hit's normal, position and material albedo; zero when the camera ray misses) */
+typedef struct { f3 normal, pos, albedo; int set; } feat_t;
 
 static int hit_world(const scene_t* sc, ray_t r, float tMin, float tMax, hit_t* outHit, int* outID) { /* parallel.cpp:54-73 */
     hit_t tmp;
@@ -224,7 +229,12 @@ static int scatter(const scene_t* sc, int matID, ray_t r_in, const hit_t* rec, f
     return 1;
 }
 
-static f3 trace(const scene_t* sc, ray_t r, int depth, long long* rays, uint32_t* rng) {   /* parallel.cpp:200-227 */
+/* prevLambert / sc->noDoubleLight: the GL loop's doMaterialE (fragmentShader.fs.glsl:430,
+ * 456-457) -- a scatter event reached through a Lambert bounce does not add its emissive
+ * again (that light was sampled explicitly); the terminating hit always adds it. The
+ * accumulation stays the CPU reference's recursion (parallel.cpp:214). */
+static f3 trace(const scene_t* sc, ray_t r, int depth, long long* rays, uint32_t* rng, int prevLambert,
+                feat_t* feat) {   /* parallel.cpp:200-227 */
     hit_t rec;
     int id = 0;
     ++*rays;
@@ -232,8 +242,16 @@ static f3 trace(const scene_t* sc, ray_t r, int depth, long long* rays, uint32_t
         ray_t scattered;
         f3 attenuation, lightE;
         f3 matE = sc->mats[id].emissive;
-        if (depth < sc->maxDepth && scatter(sc, id, r, &rec, &attenuation, &scattered, &lightE, rays, rng))
-            return add(add(matE, lightE), mul(attenuation, trace(sc, scattered, depth + 1, rays, rng)));
+        if (feat) {
+            feat->normal = rec.normal;
+            feat->pos = rec.pos;
+            feat->albedo = sc->mats[id].albedo;
+        }
+        if (depth < sc->maxDepth && scatter(sc, id, r, &rec, &attenuation, &scattered, &lightE, rays, rng)) {
+            if (sc->noDoubleLight && prevLambert) matE = v3(0.0f, 0.0f, 0.0f);
+            return add(add(matE, lightE), mul(attenuation, trace(sc, scattered, depth + 1, rays, rng,
+                                                                 sc->mats[id].type == 0, NULL)));
+        }
         return matE;
     }
     f3 unitDir = r.dir;
@@ -297,20 +315,64 @@ int orc_hit_sphere(const float* o, const float* d, const float* sph, float tMin,
 }
 
 /* ---- per-pixel body of TraceRowJob (parallel.cpp:270-286) ---- */
+/* AdaptiveStdvar (fragmentShader.fs.glsl:494-497) with pow(x, 2) as x * x (GLSL's pow is
+ * undefined for the negative differences it is given) */
+static inline float adaptive_std(float lastStd, float lastMean, int n, float newVal, float newMean) {
+    float nf = (float)n;
+    float dm = lastMean - newMean, dv = newVal - newMean;
+    return sqrtf((nf * (lastStd * lastStd) + nf * (dm * dm) + dv * dv) / (float)(n + 1));
+}
+
+/* feature buffers (each RGBA-stride like the backbuffer, any may be NULL) */
+typedef struct { float *normal, *pos, *albedo, *color_std, *normal_std, *pos_std; int max_frame; } feats_t;
+
+static inline void lerp3(float* px, f3 v, float lerpFac) {   /* parallel.cpp:282's lerp on a feature */
+    f3 prev = v3(px[0], px[1], px[2]);
+    f3 c = add(mulf(prev, lerpFac), mulf(v, 1.0f - lerpFac));
+    px[0] = c.x; px[1] = c.y; px[2] = c.z;
+}
+static inline void std3(float* sd, const float* lastMean, const float* newMean, f3 v, int n) {
+    float nv[3] = {v.x, v.y, v.z};
+    for (int k = 0; k < 3; ++k) sd[k] = adaptive_std(sd[k], lastMean[k], n, nv[k], newMean[k]);
+}
+
 static inline void shade_pixel(const scene_t* sc, const cam_t* cam, int w, int h, int x, int y, int frame,
-                               uint32_t* rng, float* pix, long long* rays) {
+                               uint32_t* rng, float* pix, long long* rays, const feats_t* fb, size_t off) {
     float invWidth = 1.0f / (float)w;                                              /* :260 */
     float invHeight = 1.0f / (float)h;                                             /* :261 */
     float lerpFac = (float)frame / (float)(frame + 1);                             /* :262 */
     float u = ((float)x + orc_random01(rng)) * invWidth;                           /* :272 */
     float v = ((float)y + orc_random01(rng)) * invHeight;                          /* :273 */
     ray_t r = get_ray(cam, u, v, rng);
-    f3 col = trace(sc, r, 0, rays, rng);
+    feat_t feat;
+    memset(&feat, 0, sizeof(feat));
+    const int doFeat = fb && (fb->max_frame < 0 || frame <= fb->max_frame);
+    f3 sample = trace(sc, r, 0, rays, rng, 0, doFeat ? &feat : NULL);
     f3 prev = v3(pix[0], pix[1], pix[2]);
-    col = add(mulf(prev, lerpFac), mulf(col, 1.0f - lerpFac));                     /* :282 */
+    f3 col = add(mulf(prev, lerpFac), mulf(sample, 1.0f - lerpFac));               /* :282 */
     pix[0] = col.x;
     pix[1] = col.y;
     pix[2] = col.z;
+    if (!doFeat) return;
+    /* fragmentShader.fs.glsl:536-568: lerp the features like the colour, then update the
+     * running std-devs from the previous and new means */
+    const float lastC[3] = {prev.x, prev.y, prev.z}, newC[3] = {col.x, col.y, col.z};
+    if (fb->color_std) std3(fb->color_std + off, lastC, newC, sample, frame);
+    if (fb->normal || fb->normal_std) {
+        float tmp[4] = {0, 0, 0, 0};
+        float* m = fb->normal ? fb->normal + off : tmp;
+        float last[3] = {m[0], m[1], m[2]};
+        lerp3(m, feat.normal, lerpFac);
+        if (fb->normal_std) std3(fb->normal_std + off, last, m, feat.normal, frame);
+    }
+    if (fb->pos || fb->pos_std) {
+        float tmp[4] = {0, 0, 0, 0};
+        float* m = fb->pos ? fb->pos + off : tmp;
+        float last[3] = {m[0], m[1], m[2]};
+        lerp3(m, feat.pos, lerpFac);
+        if (fb->pos_std) std3(fb->pos_std + off, last, m, feat.pos, frame);
+    }
+    if (fb->albedo) lerp3(fb->albedo + off, feat.albedo, lerpFac);
 }
 
 static inline uint32_t pixel_seed(uint32_t x, uint32_t y, uint32_t f) {
@@ -322,6 +384,7 @@ typedef struct {
     cam_t cam;
     int w, h, x0, xc, y0, yc, frame0, frames;
     float* buf;
+    const feats_t* fb;
     int next_row;            /* shared row cursor (atomic) */
     long long rays;          /* per-thread slot below */
 } job_t;
@@ -339,7 +402,8 @@ static void* worker(void* arg) {
             int x = j->x0 + lx, y = j->y0 + ly;
             for (int f = j->frame0; f < j->frame0 + j->frames; ++f) {
                 uint32_t rng = pixel_seed((uint32_t)x, (uint32_t)y, (uint32_t)f);
-                shade_pixel(&j->sc, &j->cam, j->w, j->h, x, y, f, &rng, pix, &wk->rays);
+                shade_pixel(&j->sc, &j->cam, j->w, j->h, x, y, f, &rng, pix, &wk->rays, j->fb,
+                            ((size_t)ly * j->xc + lx) * 4);
             }
         }
     }
@@ -364,15 +428,31 @@ static void load_scene(scene_t* sc, const float* spheres, const float* mats, int
     sc->mats = *mp;
     sc->count = count;
     sc->maxDepth = depth;
+    sc->noDoubleLight = 0;
 }
 
 long long orc_render_p(const float* spheres, const float* mats, int count, const float* cam22, int w, int h,
                        int x0, int xc, int y0, int yc, int frame0, int frames, int depth, float* buf, int threads) {
+    return orc_render_p_ex(spheres, mats, count, cam22, w, h, x0, xc, y0, yc, frame0, frames, depth, 0, buf,
+                           NULL, -1, threads);
+}
+
+long long orc_render_p_ex(const float* spheres, const float* mats, int count, const float* cam22, int w, int h,
+                          int x0, int xc, int y0, int yc, int frame0, int frames, int depth, int flags, float* buf,
+                          float* const* feats, int max_frame, int threads) {
     job_t j;
+    feats_t fb;
     sphere_t* sp;
     mat_t* mp;
     memset(&j, 0, sizeof(j));
     load_scene(&j.sc, spheres, mats, count, depth, &sp, &mp);
+    j.sc.noDoubleLight = (flags & ORC_NO_DOUBLE_LIGHT) != 0;
+    if (feats) {
+        fb.normal = feats[0]; fb.pos = feats[1]; fb.albedo = feats[2];
+        fb.color_std = feats[3]; fb.normal_std = feats[4]; fb.pos_std = feats[5];
+        fb.max_frame = max_frame;
+        j.fb = &fb;
+    }
     j.cam = cam22 ? cam_from22(cam22) : default_camera(w, h);
     j.w = w; j.h = h; j.x0 = x0; j.xc = xc; j.y0 = y0; j.yc = yc;
     j.frame0 = frame0; j.frames = frames; j.buf = buf;
@@ -401,7 +481,7 @@ long long orc_render_r(const float* spheres, const float* mats, int count, int w
     for (int f = frame0; f < frame0 + frames; ++f)
         for (int y = 0; y < h; ++y)
             for (int x = 0; x < w; ++x)
-                shade_pixel(&sc, &cam, w, h, x, y, f, state, buf + ((size_t)y * w + x) * 4, &rays);
+                shade_pixel(&sc, &cam, w, h, x, y, f, state, buf + ((size_t)y * w + x) * 4, &rays, NULL, 0);
     free(sp); free(mp);
     return rays;
 }

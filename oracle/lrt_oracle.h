@@ -45,6 +45,18 @@ long long orc_render_p(const float* spheres, const float* mats, int count, const
                        int w, int h, int x0, int xc, int y0, int yc, int frame0, int frames,
                        int depth, float* buf, int threads);
 
+/* orc_render_p plus the GL path's opt-in features (fragmentShader.fs.glsl):
+ * flags & ORC_NO_DOUBLE_LIGHT: doMaterialE rule (:430,456-457) on the CPU recursion;
+ * feats[6] (NULL: none; entries may be NULL): first-hit normal, world position and
+ * albedo running means, and running std-devs of colour, normal and world position
+ * (:444-451, :494-568), each xc*yc*4 floats like buf, updated for frames
+ * f <= max_frame (GL: 4; < 0: all). */
+#define ORC_NO_DOUBLE_LIGHT 64
+long long orc_render_p_ex(const float* spheres, const float* mats, int count, const float* cam22,
+                          int w, int h, int x0, int xc, int y0, int yc, int frame0, int frames,
+                          int depth, int flags, float* buf, float* const* feats, int max_frame,
+                          int threads);
+
 /* Mode R: the reference stream (one RNG from *state, rows in order). */
 long long orc_render_r(const float* spheres, const float* mats, int count, int w, int h,
                        int frame0, int frames, int depth, uint32_t* state, float* buf);

@@ -44,6 +44,9 @@ def orc():
         lib = ctypes.CDLL(ORC_PATH)
         lib.orc_render_p.restype = _ll
         lib.orc_render_p.argtypes = [_P, _P, ctypes.c_int, _P] + [ctypes.c_int] * 9 + [_P, ctypes.c_int]
+        lib.orc_render_p_ex.restype = _ll
+        lib.orc_render_p_ex.argtypes = ([_P, _P, ctypes.c_int, _P] + [ctypes.c_int] * 10 +
+                                        [_P, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int])
         lib.orc_render_r.restype = _ll
         lib.orc_render_r.argtypes = [_P, _P] + [ctypes.c_int] * 6 + [ctypes.POINTER(ctypes.c_uint32), _P]
         lib.orc_libm_eval.restype = None
@@ -116,6 +119,36 @@ def orc_render(width, height, frames=1, depth=8, frame0=0, x0=0, xc=None, y0=0, 
     cam = None if cam22 is None else np.ascontiguousarray(cam22, np.float32)
     rays = orc().orc_render_p(_ptr(spheres), _ptr(mats), len(spheres) // 4, _ptr(cam), width, height,
                               x0, xc, y0, yc, frame0, frames, depth, _ptr(buf), threads)
+    return buf, rays
+
+
+FEATURE_NAMES = ("normal", "world_pos", "albedo", "color_std", "normal_std", "world_pos_std")
+
+
+def orc_render_ex(width, height, frames=1, depth=8, frame0=0, x0=0, xc=None, y0=0, yc=None,
+                  spheres=None, mats=None, cam22=None, buf=None, flags=0, features=None, max_frame=4,
+                  threads=0):
+    """orc_render plus the GL path's opt-in modes: flags & 64 = no double lighting;
+    features = {name: float32 buffer[yc, xc, 4]} updated in place. Returns (buf, rays)."""
+    xc = width - x0 if xc is None else xc
+    yc = height - y0 if yc is None else yc
+    if spheres is None:
+        spheres, mats = default_scene_arrays()
+    spheres = np.ascontiguousarray(spheres, np.float32)
+    mats = np.ascontiguousarray(mats, np.float32)
+    if buf is None:
+        buf = np.zeros((yc, xc, 4), np.float32)
+    cam = None if cam22 is None else np.ascontiguousarray(cam22, np.float32)
+    fp = None
+    if features is not None:
+        fp = (ctypes.c_void_p * 6)()
+        for i, name in enumerate(FEATURE_NAMES):
+            b = features.get(name)
+            if b is not None:
+                assert b.dtype == np.float32 and b.flags.c_contiguous and b.size == yc * xc * 4
+                fp[i] = b.ctypes.data
+    rays = orc().orc_render_p_ex(_ptr(spheres), _ptr(mats), len(spheres) // 4, _ptr(cam), width, height,
+                                 x0, xc, y0, yc, frame0, frames, depth, flags, _ptr(buf), fp, max_frame, threads)
     return buf, rays
 
 
