@@ -119,19 +119,33 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 template <int MAXD, bool kLds, bool kBvh, int kSplit, bool kFeat = false>
 __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(const KernelArgs a) {
     static_assert(!kFeat || kSplit == 1, "feature launches keep a pixel's frames on one lane");
-    // LDS: [recursion stack kTraceLdsLevels x kBlock][spheres][materials][lights][bvh stack]
+    // LDS: [recursion stack kTraceLdsLevels x kBlock][powf tables][spheres][materials][lights][bvh stack]
     extern __shared__ float4 smem[];
     const int tid = threadIdx.x;
-    float4* s_sph = smem + kTraceLdsLevels * kBlock;
+    // powf tables (Dielectric's schlick): a per-lane gather from global memory costs a
+    // VMEM round trip per lookup, and vmcnt retires in order behind the tile fetch
+    double* s_pow = reinterpret_cast<double*>(smem + kTraceLdsLevels * kBlock);
+    {
+        const libm::PowTables g = libm::pow_tables();
+        for (int i = tid; i < 16; i += kBlock) {
+            s_pow[i] = g.invc[i];
+            s_pow[16 + i] = g.logc[i];
+        }
+        for (int i = tid; i < 32; i += kBlock) reinterpret_cast<uint64_t*>(s_pow + 32)[i] = g.exp2[i];
+    }
+    float4* s_sph = smem + kTraceLdsLevels * kBlock + kPowTableBytes / 16;
     float4* s_mat = s_sph + a.count;
     int* s_lights = reinterpret_cast<int*>(s_mat + 3 * a.count);
     if (kLds) {
         for (int i = tid; i < a.count; i += kBlock) s_sph[i] = a.sph[i];
         for (int i = tid; i < 3 * a.count; i += kBlock) s_mat[i] = a.mats[i];
         for (int i = tid; i < a.nlights; i += kBlock) s_lights[i] = a.lights[i];
-        __syncthreads();
     }
+    __syncthreads();
     SceneView sc;
+    sc.pow.invc = s_pow;
+    sc.pow.logc = s_pow + 16;
+    sc.pow.exp2 = reinterpret_cast<const uint64_t*>(s_pow + 32);
     sc.sph = kLds ? s_sph : a.sph;
     sc.mats = kLds ? s_mat : a.mats;
     sc.lights = kLds ? s_lights : a.lights;
@@ -141,7 +155,14 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
     sc.bstk = reinterpret_cast<unsigned short*>(reinterpret_cast<char*>(smem) + a.bvh_stack_offset) + tid;
     sc.bstride = kBlock;
 #ifdef LRT_EXP_SECSTATS
+    __shared__ unsigned long long s_sectime[kBlock / 64][2 + kSecN];
     sc.secstats = a.wtrace;
+    sc.sectime = s_sectime[tid >> 6];
+    if ((tid & 63) == 0) {
+        for (int k = 0; k < 2 + kSecN; ++k) sc.sectime[k] = 0;
+        sc.sectime[0] = kSecOther;
+        sc.sectime[1] = __builtin_amdgcn_s_memtime();
+    }
 #endif
 #ifdef LRT_EXP_WAVETRACE
     const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
@@ -167,10 +188,10 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
     for (int i = blockIdx.x / kV0Queues; i < nq;) {
         // Block b starts on its queue's tile b / kV0Queues; later tiles come from the
         // queue's counter (zeroed by rays_collect_kernel after the launch). The fetch is
-        // issued here and consumed after the tile, so its latency hides behind the trace.
+        // issued after this tile's loads (vmcnt retires in order, so a load issued behind
+        // the atomic would wait for it) and consumed after the trace, which hides it.
+        // (Prefetching the next tile's pixels as well costs VGPRs beyond the 128 cap.)
         const int tile = q + kV0Queues * i;
-        unsigned long long fetched = 0;
-        if (LRT_V0_DYNAMIC && lane == 0) fetched = atomicAdd(ctr, 1ull);
         const int lx = (tile % tilesX) * kTileX + (wave % kBlockWavesX) * 8 + (p & 7);
         const int ly = (tile / tilesX) * kTileRows + (wave / kBlockWavesX) * kWaveRows + (p >> 3);
         const bool valid = lx < a.xc && ly < a.rows;
@@ -185,6 +206,8 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
             for (int k = 0; k < 6; ++k)
                 fb[k] = (valid && a.feat[k]) ? a.feat[k][pix] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         }
+        unsigned long long fetched = 0;
+        if (LRT_V0_DYNAMIC && lane == 0) fetched = atomicAdd(ctr, 1ull);
         for (int f0 = a.frame0; f0 < fend; f0 += kSplit) {
             const int f = f0 + sub;
             F3 col = f3(0.0f, 0.0f, 0.0f);
@@ -244,6 +267,11 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
     unsigned long long total = wave_sum((unsigned long long)rays);
     if (lane == 0) s_rays[wave] = total;
     __syncthreads();
+#ifdef LRT_EXP_SECSTATS
+    sec_enter(sc, kSecOther, false);
+    if (lane == 0)
+        for (int k = 0; k < kSecN; ++k) atomicAdd(sc.secstats + 3 * (k + kSecN * (blockIdx.x & 15)) + 2, sc.sectime[2 + k]);
+#endif
 #ifdef LRT_EXP_WAVETRACE
     if (lane == 0) {
         const size_t w = gtid >> 6;
@@ -343,6 +371,7 @@ struct Context {
     float bvh_margin = 0.0f;
     int bvh_nodes = 0;
     int bvh_on = 0, bvh_big0 = 0, bvh_nbig = 0;
+    int bvh_stack_levels = kBvhStackLevels;   // this scene's traversal depth (<= kBvhStackLevels)
 
     float* d_frame = nullptr;   // lrt_draw_test / lrt_render_host staging
     float* d_feat[6] = {};      // lrt_render_host_ex feature staging
@@ -400,6 +429,7 @@ struct BvhBuilder {
     std::vector<float4> nodes, lsph;
     std::vector<int> lid;
     const std::vector<float4>* sph = nullptr;
+    int max_depth = 0;   // deepest internal node (root = 0)
 
     static void bounds(const BvhPrim* p, int n, float lo[3], float hi[3]) {
         for (int k = 0; k < 3; ++k) {
@@ -413,6 +443,7 @@ struct BvhBuilder {
             }
     }
     int node(int begin, int end, int depth) {
+        max_depth = std::max(max_depth, depth);
         const int idx = (int)(nodes.size() / 4);
         nodes.resize(nodes.size() + 4);
         const int n = end - begin;
@@ -466,6 +497,7 @@ struct BvhHost {
     std::vector<int> lid;
     int big0 = 0, nbig = 0;
     float margin = 0.0f;
+    int stack_levels = 1;   // traversal stack entries needed: one deferred sibling per level
 };
 
 // Spheres far larger than the typical one (the ground, r = 100) stay out of the tree and
@@ -512,6 +544,7 @@ void build_bvh_host(const lrt_sphere* s, int n, const std::vector<float4>& sph, 
     out.lsph.swap(B.lsph);
     out.lid.swap(B.lid);
     out.margin = 1e-5f * extent + 1e-4f;
+    out.stack_levels = B.max_depth + 1;
 }
 
 void free_scene(Context& c) {
@@ -572,6 +605,7 @@ int upload_scene(Context& c, const lrt_sphere* s, const lrt_material* m, int n) 
         c.bvh_big0 = B.big0;
         c.bvh_nbig = B.nbig;
         c.bvh_margin = B.margin;
+        c.bvh_stack_levels = B.stack_levels;
         c.bvh_on = 1;
     }
     c.count = n;
@@ -673,10 +707,12 @@ template <int MAXD, int kSplit, bool kFeat = false>
 int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     constexpr int kTileRows = kBlockWavesY * (8 / kSplit);
     const long long ntiles = (long long)((xc + kTileX - 1) / kTileX) * ((rows + kTileRows - 1) / kTileRows);
-    const size_t stack = sizeof(float4) * kTraceLdsLevels * kBlock;
+    const size_t stack = sizeof(float4) * kTraceLdsLevels * kBlock + kPowTableBytes;
     const size_t scene = lds ? sizeof(float4) * (4 * (size_t)a.count + (size_t)(a.nlights + 3) / 4 + 1) : 0;
     a.bvh_stack_offset = (int)(stack + scene);
-    const size_t bstk = a.bv.on ? sizeof(unsigned short) * kBvhStackLevels * kBlock : 0;
+    // v0 sizes the LDS traversal stack to this scene's BVH depth (1000 spheres: ~9
+    // levels, 1.2 KB instead of 3 KB per wave -- the difference between 13 and 16 waves/CU)
+    const size_t bstk = a.bv.on ? sizeof(unsigned short) * g_ctx.bvh_stack_levels * kBlock : 0;
     const size_t ldsb = stack + (lds ? scene : 0) + bstk;
     const void* kern = a.bv.on ? (lds ? (const void*)trace_kernel<MAXD, true, true, kSplit, kFeat>
                                       : (const void*)trace_kernel<MAXD, false, true, kSplit, kFeat>)
@@ -693,8 +729,8 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     a.tiles = g_ctx.d_tiles + (size_t)(g_ctx.tiles_next++ % kQueueSlots) * kTileSetU64;
 #ifdef LRT_EXP_SECSTATS
     static unsigned long long* d_sec = nullptr;
-    if (!d_sec) (void)hipMalloc(&d_sec, sizeof(unsigned long long) * 2 * kSecN * 16);
-    (void)hipMemsetAsync(d_sec, 0, sizeof(unsigned long long) * 2 * kSecN * 16, s);
+    if (!d_sec) (void)hipMalloc(&d_sec, sizeof(unsigned long long) * 3 * kSecN * 16);
+    (void)hipMemsetAsync(d_sec, 0, sizeof(unsigned long long) * 3 * kSecN * 16, s);
     a.wtrace = d_sec;
 #endif
 #ifdef LRT_EXP_WAVETRACE
@@ -726,18 +762,22 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
 #endif
 #ifdef LRT_EXP_SECSTATS
     {
-        unsigned long long h[2 * kSecN * 16];
+        unsigned long long h[3 * kSecN * 16];
         (void)hipMemcpyAsync(h, d_sec, sizeof(h), hipMemcpyDeviceToHost, s);
         (void)hipStreamSynchronize(s);
-        const char* names[kSecN] = {"hit", "lambert", "shadow", "metal", "dielectric", "fold", "camera"};
+        const char* names[kSecN] = {"hit", "lambert", "shadow", "metal", "dielectric", "post", "fold", "camera", "other"};
+        double tot = 0;
+        for (int k = 0; k < kSecN; ++k)
+            for (int j = 0; j < 16; ++j) tot += (double)h[3 * (k + kSecN * j) + 2];
         for (int k = 0; k < kSecN; ++k) {
-            unsigned long long ex = 0, ln = 0;
+            unsigned long long ex = 0, ln = 0, cy = 0;
             for (int j = 0; j < 16; ++j) {
-                ex += h[2 * (k + kSecN * j)];
-                ln += h[2 * (k + kSecN * j) + 1];
+                ex += h[3 * (k + kSecN * j)];
+                ln += h[3 * (k + kSecN * j) + 1];
+                cy += h[3 * (k + kSecN * j) + 2];
             }
-            fprintf(stderr, "secstats %-10s wave-execs %12llu  lanes %14llu  lanes/exec %6.2f\n", names[k], ex, ln,
-                    ex ? (double)ln / ex : 0.0);
+            fprintf(stderr, "secstats %-10s wave-execs %12llu  lanes/exec %6.2f  cycles %5.1f%%  cyc/exec %8.1f\n", names[k], ex,
+                    ex ? (double)ln / ex : 0.0, 100.0 * cy / tot, ex ? (double)cy / ex : 0.0);
         }
     }
 #endif

@@ -101,7 +101,11 @@ LRT_DEV F3 RandomInUnitSphere(uint32_t& s) {
         float b = RandomFloat01(s);
         float c = RandomFloat01(s);
         p = 2.0f * f3(a, b, c) - f3(1.0f, 1.0f, 1.0f);
-    } while (length(p) >= 1.0f);
+        // the reference tests p.length() >= 1.0 (maths.cpp:47). With s = x*x + y*y + z*z
+        // summed in the same order, the correctly rounded sqrt(s) >= 1 iff s >= 1:
+        // sqrt(1 - 2^-24) = 1 - 2^-25 - 2^-51 rounds down to 1 - 2^-24, and sqrt is
+        // monotonic, so the sqrt can go
+    } while (p.x * p.x + p.y * p.y + p.z * p.z >= 1.0f);
     return p;
 }
 
@@ -146,27 +150,41 @@ struct SceneView {
     BvhView bv;                        // bv.on: closest hit by BVH traversal
     unsigned short* bstk;              // this lane's BVH traversal stack (LDS)
     int bstride;
+    libm::PowTables pow;               // powf tables for Dielectric's schlick (LDS copy)
 #ifdef LRT_EXP_SECSTATS
-    unsigned long long* secstats;      // diagnostic: per section {wave executions, active lanes}
+    unsigned long long* secstats;      // diagnostic: per section {wave executions, active lanes, cycles}
+    unsigned long long* sectime;       // this wave's LDS bookkeeping
 #endif
 };
 
-// Diagnostic builds only (LRT_EXP_SECSTATS): count how many lanes are active each time a
-// wave enters section `sec` (lane utilisation per section).
-enum { kSecHit, kSecLambert, kSecShadow, kSecMetal, kSecDiel, kSecFold, kSecCamera, kSecN };
-LRT_DEV void sec_count(const SceneView& sc, int sec) {
+// Diagnostic builds only (LRT_EXP_SECSTATS): per section, how many times a wave enters
+// it, how many lanes are active then, and the shader cycles spent in it until the next
+// section switch (s_memtime, bookkept in LDS by the first active lane so divergence
+// cannot desynchronise it). sec_count enters and counts; sec_enter only switches time.
+enum { kSecHit, kSecLambert, kSecShadow, kSecMetal, kSecDiel, kSecPost, kSecFold, kSecCamera, kSecOther, kSecN };
+LRT_DEV void sec_enter(const SceneView& sc, int sec, bool count) {
 #if defined(LRT_EXP_SECSTATS) && defined(__HIP_DEVICE_COMPILE__)
     const unsigned long long m = __ballot(1);
     if ((int)__lane_id() == __ffsll((long long)m) - 1) {
-        unsigned long long* g = sc.secstats + 2 * (sec + kSecN * (blockIdx.x & 15));
-        atomicAdd(g, 1ull);
-        atomicAdd(g + 1, (unsigned long long)__popcll(m));
+        const unsigned long long now = __builtin_amdgcn_s_memtime();
+        unsigned long long* w = sc.sectime;   // LDS, this wave: [0] section, [1] since, [2 + s] cycles
+        const int cur = (int)w[0];
+        w[2 + cur] += now - w[1];
+        w[0] = (unsigned long long)sec;
+        w[1] = now;
+        if (count) {
+            unsigned long long* g = sc.secstats + 3 * (sec + kSecN * (blockIdx.x & 15));
+            atomicAdd(g, 1ull);
+            atomicAdd(g + 1, (unsigned long long)__popcll(m));
+        }
     }
 #else
     (void)sc;
     (void)sec;
+    (void)count;
 #endif
 }
+LRT_DEV void sec_count(const SceneView& sc, int sec) { sec_enter(sc, sec, true); }
 
 // HitWorld + HitSphere (parallel.cpp:54-73, maths.cpp:51-94). The per-sphere test
 // is the reference's; hit position and normal are computed once for the winner
@@ -257,7 +275,9 @@ LRT_DEV F3 ScatterDir(const Material& mat, int matId, const Ray& r_in, const Hit
             float tLight;
             ++inoutRayCount;                                                              // :122
             sec_count(sc, kSecShadow);
-            if (ClosestHitSV<kBvh>(make_ray(rec.pos, l), kMinT, kMaxT, sc, tLight) == i) {   // HitWorld && hitID == i
+            const int shadowId = ClosestHitSV<kBvh>(make_ray(rec.pos, l), kMinT, kMaxT, sc, tLight);
+            sec_enter(sc, kSecLambert, false);
+            if (shadowId == i) {   // HitWorld && hitID == i
                 float omega = 2.0f * kPI * (1.0f - cosAMax);
                 F3 rdir = r_in.dir;
                 F3 nl = dot(rec.normal, rdir) < 0.0f ? rec.normal : -rec.normal;
@@ -292,7 +312,7 @@ LRT_DEV F3 ScatterDir(const Material& mat, int matId, const Ray& r_in, const Hit
         cosine = -dot(rdir, rec.normal);
     }
     if (refract(rdir, outwardN, nint, refr))
-        reflProb = schlick(cosine, mat.ri);
+        reflProb = schlick(cosine, mat.ri, sc.pow);
     else
         reflProb = 1.0f;
     return RandomFloat01(rng) < reflProb ? refl : refr;
@@ -346,6 +366,7 @@ LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const S
         if (depth < maxDepth) {   // :212
             F3 lightE;
             const F3 X = ScatterDir<kBvh>(mat, id, r, rec, lightE, inoutRayCount, rng, sc);
+            sec_count(sc, kSecPost);
             const F3 dir = normalize(normalize(X));
             if (mat.type != 1 || dot(dir, rec.normal) > 0.0f) {   // Metal absorbs (:147)
                 if (ndl && prevLambert) matE = f3(0.0f, 0.0f, 0.0f);
@@ -368,6 +389,7 @@ LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const S
         float4 b = sc.mats[3 * __float_as_int(s.w) + 2];
         T = f3(s.x, s.y, s.z) + f3(b.x, b.y, b.z) * T;
     }
+    sec_enter(sc, kSecOther, false);
     return T;
 }
 

@@ -96,3 +96,13 @@ def test_exhaustive_sweeps():
             x = (u | np.uint32(sgn)).view(np.float32)
             assert_same(0, x)
             assert_same(1, x)
+
+
+def test_unit_sphere_rejection_without_sqrt():
+    """RandomInUnitSphere's `p.length() >= 1.0` (maths.cpp:47) is evaluated on the device
+    as `x*x + y*y + z*z >= 1` (lrt_trace.h): with IEEE correctly rounded sqrt the two
+    agree on every float s (sqrt is monotonic; the only boundary is just below 1).
+    Checked on every float in [0.5, 2]."""
+    lo, hi = np.float32(0.5).view(np.uint32), np.float32(2.0).view(np.uint32)
+    s = np.arange(lo, hi + 1, dtype=np.uint32).view(np.float32)
+    assert not np.any((np.sqrt(s) >= np.float32(1.0)) != (s >= np.float32(1.0)))
