@@ -147,6 +147,7 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
     sc.pow.logc = s_pow + 16;
     sc.pow.exp2 = reinterpret_cast<const uint64_t*>(s_pow + 32);
     sc.sph = kLds ? s_sph : a.sph;
+    sc.gsph = a.sph;
     sc.mats = kLds ? s_mat : a.mats;
     sc.lights = kLds ? s_lights : a.lights;
     sc.count = a.count;
@@ -155,11 +156,11 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
     sc.bstk = reinterpret_cast<unsigned short*>(reinterpret_cast<char*>(smem) + a.bvh_stack_offset) + tid;
     sc.bstride = kBlock;
 #ifdef LRT_EXP_SECSTATS
-    __shared__ unsigned long long s_sectime[kBlock / 64][2 + kSecN];
+    __shared__ unsigned long long s_sectime[kBlock / 64][2 + 3 * kSecN];
     sc.secstats = a.wtrace;
     sc.sectime = s_sectime[tid >> 6];
     if ((tid & 63) == 0) {
-        for (int k = 0; k < 2 + kSecN; ++k) sc.sectime[k] = 0;
+        for (int k = 0; k < 2 + 3 * kSecN; ++k) sc.sectime[k] = 0;
         sc.sectime[0] = kSecOther;
         sc.sectime[1] = __builtin_amdgcn_s_memtime();
     }
@@ -270,7 +271,12 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
 #ifdef LRT_EXP_SECSTATS
     sec_enter(sc, kSecOther, false);
     if (lane == 0)
-        for (int k = 0; k < kSecN; ++k) atomicAdd(sc.secstats + 3 * (k + kSecN * (blockIdx.x & 15)) + 2, sc.sectime[2 + k]);
+        for (int k = 0; k < kSecN; ++k) {
+            unsigned long long* g = sc.secstats + 3 * (k + kSecN * (blockIdx.x & 15));
+            atomicAdd(g, sc.sectime[2 + kSecN + k]);
+            atomicAdd(g + 1, sc.sectime[2 + 2 * kSecN + k]);
+            atomicAdd(g + 2, sc.sectime[2 + k]);
+        }
 #endif
 #ifdef LRT_EXP_WAVETRACE
     if (lane == 0) {
@@ -812,7 +818,7 @@ int launch_paths(PathArgs& a, hipStream_t s) {
     long long blocks = (long long)per_cu * g_ctx.num_cus;
     if (blocks > want) blocks = want;
     dim3 grid((unsigned)blocks);
-    if (kStaticPixel) {   // kPix pixels per lane: 16 x 16*kPix tiles, no persistence
+    if constexpr (kStaticPixel) {   // kPix pixels per lane: 16 x 16*kPix tiles, no persistence
         grid = dim3((unsigned)((a.xc + 15) / 16), (unsigned)((a.rows + 16 * kPix - 1) / (16 * kPix)));
         blocks = (long long)grid.x * grid.y;
     }

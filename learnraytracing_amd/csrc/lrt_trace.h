@@ -141,8 +141,17 @@ LRT_DEV Material load_material(const float4* __restrict__ mats, int id) {
 #include "lrt_bvh.h"
 namespace lrt {
 
+// LRT_SCALAR_SCENE=1: the linear closest-hit scan (uniform sphere index) reads spheres
+// through the constant address space, i.e. scalar loads into SGPRs, instead of LDS.
+// Measured slower than the LDS broadcast reads (config 2: 0.409 vs 0.394 ms), so off.
+#ifndef LRT_SCALAR_SCENE
+#define LRT_SCALAR_SCENE 0
+#endif
+typedef const __attribute__((address_space(4))) float* ConstFPtr;
+
 struct SceneView {
     const float4* sph;                 // LDS or global
+    const float4* gsph;                // the same spheres in global memory (scalar loads)
     const float4* __restrict__ mats;   // global (per-lane gather, L1/L2 resident)
     const int* __restrict__ lights;    // emissive sphere ids in index order
     int count;
@@ -167,15 +176,17 @@ LRT_DEV void sec_enter(const SceneView& sc, int sec, bool count) {
     const unsigned long long m = __ballot(1);
     if ((int)__lane_id() == __ffsll((long long)m) - 1) {
         const unsigned long long now = __builtin_amdgcn_s_memtime();
-        unsigned long long* w = sc.sectime;   // LDS, this wave: [0] section, [1] since, [2 + s] cycles
+        // LDS, this wave: [0] section, [1] since, [2 + s] cycles, [2 + kSecN + s] entries,
+        // [2 + 2 kSecN + s] active lanes -- no global atomics in the loop (they would sit
+        // in vmcnt and be charged to whichever section waits next)
+        unsigned long long* w = sc.sectime;
         const int cur = (int)w[0];
         w[2 + cur] += now - w[1];
         w[0] = (unsigned long long)sec;
         w[1] = now;
         if (count) {
-            unsigned long long* g = sc.secstats + 3 * (sec + kSecN * (blockIdx.x & 15));
-            atomicAdd(g, 1ull);
-            atomicAdd(g + 1, (unsigned long long)__popcll(m));
+            w[2 + kSecN + sec] += 1;
+            w[2 + 2 * kSecN + sec] += (unsigned long long)__popcll(m);
         }
     }
 #else
@@ -195,10 +206,12 @@ LRT_DEV int ClosestHitSV(const Ray& r, float tMin, float tMax, const SceneView& 
     if (kBvh) return ClosestHitBVH(r.orig, r.dir, sc.bv, tOut, sc.bstk, sc.bstride);   // tMin/tMax = kMinT/kMaxT
     float closestT = tMax;
     int id = -1;
-    float4 next = sc.sph[0];
+    const ConstFPtr csph = (ConstFPtr)sc.gsph;
+    auto cload = [&](int i) { return make_float4(csph[4 * i], csph[4 * i + 1], csph[4 * i + 2], csph[4 * i + 3]); };
+    float4 next = LRT_SCALAR_SCENE ? cload(0) : sc.sph[0];   // one sphere ahead (SGPRs or VGPRs)
     for (int i = 0; i < sc.count; ++i) {
         const float4 s = next;
-        if (i + 1 < sc.count) next = sc.sph[i + 1];
+        if (i + 1 < sc.count) next = LRT_SCALAR_SCENE ? cload(i + 1) : sc.sph[i + 1];
         F3 rs = f3(s.x, s.y, s.z) - r.orig;
         float rsProj = dot(rs, r.dir);
         float ifHit = dot(rs, rs) - rsProj * rsProj - s.w;
