@@ -254,9 +254,20 @@ LRT_DEV bool HitWorld(const Ray& r, float tMin, float tMax, const SceneView& sc,
 // caller forms the ray once for whichever materials the wave's lanes hold; Metal's
 // absorption test (:147) is applied there too. The attenuation is the material's
 // `att` row (albedo or 1), read back by the fold.
+// The last light sample of a Lambert scatter, left for the caller to trace together with
+// the next bounce ray (TraceDual): its direction, light index and the contribution
+// (mat.albedo * emissive) * (max(0, l.nl) * omega / pi) it adds if the shadow ray's
+// closest hit is that light (parallel.cpp:122-132; a pure function of values known
+// before the shadow test, so precomputing it changes no bits).
+struct DeferredLight {
+    F3 l, contrib;   // l: the shadow ray's direction
+    int li;
+    bool on;
+};
+
 template <bool kBvh = false>
 LRT_DEV F3 ScatterDir(const Material& mat, int matId, const Ray& r_in, const Hit& rec, F3& outLightE,
-                      int& inoutRayCount, uint32_t& rng, const SceneView& sc) {
+                      int& inoutRayCount, uint32_t& rng, const SceneView& sc, DeferredLight* defer = nullptr) {
     outLightE = f3(0.0f, 0.0f, 0.0f);
     if (mat.type == 0) {  // Lambert :81-136
         sec_count(sc, kSecLambert);
@@ -287,6 +298,19 @@ LRT_DEV F3 ScatterDir(const Material& mat, int matId, const Ray& r_in, const Hit
             l = normalize_member(l);                                                      // :117
             float tLight;
             ++inoutRayCount;                                                              // :122
+            if (defer && k == sc.nlights - 1) {   // the last light: traced with the bounce ray
+                float omega = 2.0f * kPI * (1.0f - cosAMax);
+                F3 rdir = r_in.dir;
+                F3 nl = dot(rec.normal, rdir) < 0.0f ? rec.normal : -rec.normal;
+                float d = dot(l, nl);
+                float mx = (0.0f < d) ? d : 0.0f;   // std::max(0.0f, d)
+                const float4 e = sc.mats[3 * i + 1];
+                defer->l = normalize(l);   // the shadow Ray's ctor normalises again (maths.h:133-137)
+                defer->contrib = (mat.albedo * f3(e.x, e.y, e.z)) * (mx * omega / kPI);
+                defer->li = i;
+                defer->on = true;
+                continue;
+            }
             sec_count(sc, kSecShadow);
             const int shadowId = ClosestHitSV<kBvh>(make_ray(rec.pos, l), kMinT, kMaxT, sc, tLight);
             sec_enter(sc, kSecLambert, false);
@@ -342,6 +366,12 @@ LRT_DEV F3 ScatterDir(const Material& mat, int matId, const Ray& r_in, const Hit
 #define LRT_TRACE_LDS_LEVELS 8
 #endif
 constexpr int kTraceLdsLevels = LRT_TRACE_LDS_LEVELS;
+#ifndef LRT_DUAL_HIT
+#define LRT_DUAL_HIT 1
+#endif
+template <int MAXD, bool kFeat, int kLdsLev>
+LRT_DEV F3 TraceDual(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const SceneView& sc,
+                     float4* lstk, int lstride, float4* gstk, size_t gstride, int ndl, F3* feat);
 // ndl (LRT_F_NO_DOUBLE_LIGHT): the GL loop's doMaterialE rule (fragmentShader.fs.glsl:430,
 // 456-457) -- a scatter event reached through a Lambert bounce adds no emissive; the
 // terminating hit always does. kFeat: feat[0..2] receive the first hit's normal,
@@ -349,6 +379,9 @@ constexpr int kTraceLdsLevels = LRT_TRACE_LDS_LEVELS;
 template <int MAXD, bool kBvh = false, bool kFeat = false, int kLdsLev = kTraceLdsLevels>
 LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const SceneView& sc,
                  float4* lstk, int lstride, float4* gstk, size_t gstride, int ndl = 0, F3* feat = nullptr) {
+    if constexpr (!kBvh && LRT_DUAL_HIT)
+        return TraceDual<MAXD, kFeat, kLdsLev>(r, maxDepth, inoutRayCount, rng, sc, lstk, lstride, gstk, gstride,
+                                               ndl, feat);
     auto put = [&](int lvl, float4 v) {
         if (MAXD <= kLdsLev || lvl < kLdsLev) lstk[lvl * lstride] = v;
         else gstk[(size_t)(lvl - kLdsLev) * gstride] = v;
@@ -389,6 +422,144 @@ LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const S
                 ++depth;
                 r.orig = rec.pos;
                 r.dir = dir;
+                continue;
+            }
+        }
+        leaf = matE;
+        break;
+    }
+    F3 T = leaf;
+    sec_count(sc, kSecFold);
+    for (int d = depth - 1; d >= 0; --d) {
+        float4 s = get(d);
+        float4 b = sc.mats[3 * __float_as_int(s.w) + 2];
+        T = f3(s.x, s.y, s.z) + f3(b.x, b.y, b.z) * T;
+    }
+    sec_enter(sc, kSecOther, false);
+    return T;
+}
+
+// One pass over the spheres for two rays from the same origin: the next bounce ray and
+// (hasShadow) a light's shadow ray. rs = c - o and dot(rs, rs) are shared -- the very
+// values HitSphere computes for each ray (maths.cpp:54-59) -- and each ray keeps its own
+// shrinking closestT exactly as HitWorld does, so both results are bit-identical to two
+// separate scans. Saves the shadow ray's separate, partly occupied pass.
+LRT_DEV void DualClosestHit(const F3& o, const F3& db, bool hasShadow, const F3& ds, const SceneView& sc,
+                            int& idB, float& tB, int& idS) {
+    float closestB = kMaxT, closestS = kMaxT;
+    idB = -1;
+    idS = -1;
+    float4 next = sc.sph[0];
+    for (int i = 0; i < sc.count; ++i) {
+        const float4 s = next;
+        if (i + 1 < sc.count) next = sc.sph[i + 1];
+        const F3 rs = f3(s.x, s.y, s.z) - o;
+        const float rr = dot(rs, rs);
+        {
+            const float rsProj = dot(rs, db);
+            const float ifHit = rr - rsProj * rsProj - s.w;
+            if (ifHit < 0.0f) {
+                const float halfCut = __builtin_sqrtf(-ifHit);
+                float t = rsProj - halfCut;
+                if (t > kMinT && t < closestB) {
+                    closestB = t;
+                    idB = i;
+                } else {
+                    t = rsProj + halfCut;
+                    if (t > kMinT && t < closestB) {
+                        closestB = t;
+                        idB = i;
+                    }
+                }
+            }
+        }
+        if (hasShadow) {
+            const float rsProj = dot(rs, ds);
+            const float ifHit = rr - rsProj * rsProj - s.w;
+            if (ifHit < 0.0f) {
+                const float halfCut = __builtin_sqrtf(-ifHit);
+                float t = rsProj - halfCut;
+                if (t > kMinT && t < closestS) {
+                    closestS = t;
+                    idS = i;
+                } else {
+                    t = rsProj + halfCut;
+                    if (t > kMinT && t < closestS) {
+                        closestS = t;
+                        idS = i;
+                    }
+                }
+            }
+        }
+    }
+    tB = closestB;
+}
+
+// Trace for the linear scan with the closest hit of each bounce ray found at the end of
+// the previous iteration, in one pass with the last light's shadow ray (DualClosestHit).
+// Same events, draws, ray counts and accumulation order as Trace.
+template <int MAXD, bool kFeat = false, int kLdsLev = kTraceLdsLevels>
+LRT_DEV F3 TraceDual(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const SceneView& sc,
+                     float4* lstk, int lstride, float4* gstk, size_t gstride, int ndl, F3* feat) {
+    auto put = [&](int lvl, float4 v) {
+        if (MAXD <= kLdsLev || lvl < kLdsLev) lstk[lvl * lstride] = v;
+        else gstk[(size_t)(lvl - kLdsLev) * gstride] = v;
+    };
+    auto get = [&](int lvl) -> float4 {
+        if (MAXD <= kLdsLev || lvl < kLdsLev) return lstk[lvl * lstride];
+        return gstk[(size_t)(lvl - kLdsLev) * gstride];
+    };
+    int depth = 0;
+    bool prevLambert = false;
+    F3 leaf;
+    Hit rec;
+    int id = 0;
+    ++inoutRayCount;
+    bool hit = HitWorld<false>(r, kMinT, kMaxT, sc, rec, id);
+    for (;;) {
+        if (!hit) {
+            float t = 0.5f * (r.dir.y + 1.0f);
+            leaf = ((1.0f - t) * f3(1.0f, 1.0f, 1.0f) + t * f3(0.5f, 0.7f, 1.0f)) * 0.3f;
+            break;
+        }
+        Material mat = load_material(sc.mats, id);
+        F3 matE = mat.emissive;
+        if (kFeat && depth == 0) {
+            feat[0] = rec.normal;
+            feat[1] = rec.pos;
+            feat[2] = mat.albedo;
+        }
+        if (depth < maxDepth) {   // :212
+            F3 lightE;
+            DeferredLight dl;
+            dl.on = false;
+            const F3 X = ScatterDir<false>(mat, id, r, rec, lightE, inoutRayCount, rng, sc, &dl);
+            sec_count(sc, kSecPost);
+            const F3 dir = normalize(normalize(X));
+            if (mat.type != 1 || dot(dir, rec.normal) > 0.0f) {   // Metal absorbs (:147)
+                // the next Trace's HitWorld (:204) and the deferred shadow ray (:122-123)
+                ++inoutRayCount;
+                sec_count(sc, kSecHit);
+                int nid, sid;
+                float nt;
+                DualClosestHit(rec.pos, dir, dl.on, dl.l, sc, nid, nt, sid);
+                if (dl.on && sid == dl.li) lightE = lightE + dl.contrib;
+                sec_enter(sc, kSecPost, false);
+                if (ndl && prevLambert) matE = f3(0.0f, 0.0f, 0.0f);
+                prevLambert = mat.type == 0;
+                F3 e = matE + lightE;
+                put(depth, make_float4(e.x, e.y, e.z, __int_as_float(id)));
+                ++depth;
+                r.orig = rec.pos;
+                r.dir = dir;
+                hit = nid >= 0;
+                if (hit) {   // HitWorld's winner data (maths.cpp:74-76,86-88)
+                    const float4 s = sc.sph[nid];
+                    rec.pos = point_at(r, nt);
+                    rec.normal = normalize(rec.pos - f3(s.x, s.y, s.z));
+                    rec.t = nt;
+                    id = nid;
+                }
                 continue;
             }
         }
