@@ -110,6 +110,25 @@ def read_traffic(cfg_name: str):
         return None, None
 
 
+def read_valu(cfg_name: str):
+    """VALU issue fraction and lane utilisation of trace_kernel from the summary of the
+    committed PMC run that pmc_traffic.json points at (the path's real bound)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+            src = json.load(f)[cfg_name]["source"]
+        sp = os.path.join(ROOT, "profiles", src, "summary.json")
+        with open(sp) as f:
+            s = json.load(f)
+        c = s["counters_per_launch"]
+        return {"issue_frac": round(s["valu_issue_frac_of_peak"], 4),
+                "lane_util": round(c["SQ_THREAD_CYCLES_VALU"] / (c["SQ_ACTIVE_INST_VALU"] * 64), 4),
+                "note": "wave64 VALU instructions issued / (1024 SIMDs x 1 per 2 cycles at 2.4 GHz); "
+                        "lane_util = active lanes per VALU instruction / 64",
+                "source": os.path.relpath(sp, ROOT)}
+    except (OSError, ValueError, KeyError, ZeroDivisionError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -280,6 +299,7 @@ def main():
                 "note": "24 B per pixel-sample (SURVEY 8(d)); the path is VALU-bound, HBM frac is "
                         "reported as north_star asks" + (f"; traffic from {traffic_src}" if traffic_src else ""),
             },
+            "valu": read_valu(f"{cfg_name}_n{world}"),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
