@@ -209,8 +209,9 @@ int lrt_libm_eval_device(int kind, const float* d_in, float* d_out, long long n)
 
 /* BVH diagnostics (host only, no GPU): build the BVH of the given scene and trace n rays
  * (6 floats each: origin, direction) with the device traversal code. out[5]: mean nodes
- * visited, mean spheres tested, max nodes, max spheres, fraction of rays whose closest
- * hit differs from the linear scan (0 by construction). */
+ * visited, mean spheres tested, max nodes, max spheres, and mismatches per ray against
+ * the linear scan (0 by construction): closest hit (id and t), and the bounded shadow-ray
+ * traversal for the scan's winner and for one other sphere per ray. */
 int lrt_bvh_stats(const lrt_sphere* spheres, int count, const float* rays, int n, double* out);
 
 #ifdef __cplusplus

@@ -121,4 +121,70 @@ LRT_DEV int ClosestHitBVH(const F3& o, const F3& d, const BvhView& bv, float& tO
     return best;
 }
 
+// Light sampling's `HitWorld(shadow ray) && hitID == li` (parallel.cpp:122-123) through
+// the BVH. (cand_li, li) must be the lexicographic minimum, so the light's own candidate
+// is the bar from the start: boxes beyond it are culled (same conservative margins) and
+// the first sphere that beats it -- cand_j < cand_li, or equal with j < li -- ends the
+// traversal. Same per-sphere arithmetic as the scan, so the answer is bit-identical.
+LRT_DEV float SphereCand(const F3& o, const F3& d, const float4& s) {   // maths.cpp:54-90
+    const F3 rs = f3(s.x, s.y, s.z) - o;
+    const float rsProj = dot(rs, d);
+    const float ifHit = dot(rs, rs) - rsProj * rsProj - s.w;
+    if (!(ifHit < 0.0f)) return __builtin_inff();
+    const float halfCut = __builtin_sqrtf(-ifHit);
+    const float t1 = rsProj - halfCut;
+    const float t2 = rsProj + halfCut;
+    return t1 > kMinT ? t1 : (t2 > kMinT ? t2 : __builtin_inff());
+}
+LRT_DEV bool ShadowReachesLightBVH(const F3& o, const F3& d, int li, const float4& lightSph, const BvhView& bv,
+                                   unsigned short* stk, int stride) {
+    const float candL = SphereCand(o, d, lightSph);
+    if (!(candL < kMaxT)) return false;   // the light is not hit at all (closestT starts at kMaxT)
+    auto beats = [&](float c, int id) { return c < candL || (c == candL && id < li); };
+    for (int j = 0; j < bv.nbig; ++j)
+        if (beats(SphereCand(o, d, bv.lsph[bv.big0 + j]), bv.lid[bv.big0 + j])) return false;
+    if (bv.nnodes == 0) return true;
+    const F3 inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const float mb = bv.margin + 1e-5f * candL;
+    int sp = 0, cur = 0;
+    for (;;) {
+        const float4 a0 = bv.nodes[4 * cur + 0], a1 = bv.nodes[4 * cur + 1];
+        const float4 b0 = bv.nodes[4 * cur + 2], b1 = bv.nodes[4 * cur + 3];
+        float tnA, tfA, tnB, tfB;
+        SlabTest(a0, a1, o, inv, tnA, tfA);
+        SlabTest(b0, b1, o, inv, tnB, tfB);
+        const float mA = bv.margin + 1e-5f * __builtin_fabsf(tfA);
+        const float mB = bv.margin + 1e-5f * __builtin_fabsf(tfB);
+        const int cntA = lrt::libm::f2u_i(a1.w), cntB = lrt::libm::f2u_i(b1.w);
+        const bool hitA = cntA >= 0 && tnA <= tfA + mA && tnA <= candL + mb && tfA >= kMinT - mA;
+        const bool hitB = cntB >= 0 && tnB <= tfB + mB && tnB <= candL + mb && tfB >= kMinT - mB;
+        if (hitA && cntA > 0) {
+            const int ref = lrt::libm::f2u_i(a0.w);
+            for (int j = 0; j < cntA; ++j)
+                if (beats(SphereCand(o, d, bv.lsph[ref + j]), bv.lid[ref + j])) return false;
+        }
+        if (hitB && cntB > 0) {
+            const int ref = lrt::libm::f2u_i(b0.w);
+            for (int j = 0; j < cntB; ++j)
+                if (beats(SphereCand(o, d, bv.lsph[ref + j]), bv.lid[ref + j])) return false;
+        }
+        const bool goA = hitA && cntA == 0, goB = hitB && cntB == 0;
+        if (goA && goB) {
+            const bool aFirst = tnA <= tnB;
+            stk[sp * stride] = (unsigned short)lrt::libm::f2u_i(aFirst ? b0.w : a0.w);
+            ++sp;
+            cur = lrt::libm::f2u_i(aFirst ? a0.w : b0.w);
+        } else if (goA) {
+            cur = lrt::libm::f2u_i(a0.w);
+        } else if (goB) {
+            cur = lrt::libm::f2u_i(b0.w);
+        } else {
+            if (sp == 0) break;
+            --sp;
+            cur = stk[sp * stride];
+        }
+    }
+    return true;
+}
+
 }  // namespace lrt

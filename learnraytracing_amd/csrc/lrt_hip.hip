@@ -1258,6 +1258,11 @@ int lrt_bvh_stats(const lrt_sphere* spheres, int count, const float* rays, int n
         const int a = ClosestHitBVH(r.orig, r.dir, bv, t1, stk, 1, &st);
         const int b = ClosestHit(r.orig, r.dir, sph.data(), count, t2);
         if (a != b || memcmp(&t1, &t2, 4) != 0) bad += 1;
+        // the bounded shadow-ray traversal: true for the scan's winner, and for any other
+        // sphere exactly when it is the winner
+        if (b >= 0 && !ShadowReachesLightBVH(r.orig, r.dir, b, sph[b], bv, stk, 1)) bad += 1;
+        const int other = (int)(((unsigned)i * 7919u) % (unsigned)count);
+        if (ShadowReachesLightBVH(r.orig, r.dir, other, sph[other], bv, stk, 1) != (b == other)) bad += 1;
         sn += st.nodes;
         ss += st.spheres;
         mn = std::max(mn, (double)st.nodes);

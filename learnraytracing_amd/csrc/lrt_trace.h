@@ -312,9 +312,15 @@ LRT_DEV F3 ScatterDir(const Material& mat, int matId, const Ray& r_in, const Hit
                 continue;
             }
             sec_count(sc, kSecShadow);
-            const int shadowId = ClosestHitSV<kBvh>(make_ray(rec.pos, l), kMinT, kMaxT, sc, tLight);
+            bool lit;
+            if constexpr (kBvh) {
+                const Ray sr = make_ray(rec.pos, l);
+                lit = ShadowReachesLightBVH(sr.orig, sr.dir, i, s, sc.bv, sc.bstk, sc.bstride);
+            } else {
+                lit = ClosestHitSV<kBvh>(make_ray(rec.pos, l), kMinT, kMaxT, sc, tLight) == i;
+            }
             sec_enter(sc, kSecLambert, false);
-            if (shadowId == i) {   // HitWorld && hitID == i
+            if (lit) {   // HitWorld && hitID == i
                 float omega = 2.0f * kPI * (1.0f - cosAMax);
                 F3 rdir = r_in.dir;
                 F3 nl = dot(rec.normal, rdir) < 0.0f ? rec.normal : -rec.normal;
