@@ -140,6 +140,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=None, help="seconds of CPU-baseline timing")
     ap.add_argument("--scene-global", action="store_true", help="read spheres from global memory, not LDS")
+    ap.add_argument("--reserve-cus", type=int, default=None,
+                    help="CUs the render stream leaves free for other streams (default 0)")
     ap.add_argument("--kernel", choices=["auto", "v0", "v1", "v2", "v2s"], default="auto",
                     help="auto: the library's policy (default); v0: one pixel per lane (LRT_F_SIMPLE); "
                          "v1: unscheduled state machine; v2: phase-scheduled persistent; v2s[N]: "
@@ -178,6 +180,16 @@ def main():
     from learnraytracing_amd.renderer import unshard_tensor
 
     lrt.InitializeTest()
+    # --reserve-cus R: render on a CU-masked stream (lrt_stream_create) leaving R CUs to
+    # other streams. Off by default: a kernel on another stream only starts beside the
+    # persistent render once >= 8 CUs per XCD are free (64 CUs, -23 % render throughput;
+    # tools/overlap_probe.py), which costs more than the gather it would hide
+    reserve = args.reserve_cus if args.reserve_cus is not None else 0
+    rstream = None
+    if reserve > 0:
+        from learnraytracing_amd.renderer import RenderStream
+        rstream = RenderStream(reserve)
+        torch.cuda.set_stream(rstream.torch)
     if cfg["scene"] == "random1000":
         lrt.set_scene(*lrt.random_scene(1000, 1))
     W, H, D = cfg["width"], cfg["height"], cfg["depth"]
@@ -284,6 +296,7 @@ def main():
                 "parallelism": f"rows: row-block-cyclic x{world} (block {rb}), RCCL gather to rank 0"
                 if world > 1 else "single GPU",
                 "scene_reads": "global" if args.scene_global else "LDS-staged",
+                "reserved_cus": reserve,
                 "kernel": args.kernel,
             },
             "roofline": {
@@ -303,6 +316,9 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
+    if rstream is not None:
+        torch.cuda.set_stream(torch.cuda.default_stream(dev))
+        rstream.close()
     lrt.ShutdownTest()
     if world > 1:
         dist.destroy_process_group()

@@ -185,6 +185,14 @@ int lrt_render_device_ex(const lrt_render_desc* desc, float* d_backbuffer,
 int lrt_render_host_ex(const lrt_render_desc* desc, float* backbuffer, long long* out_rays,
                        const lrt_features* features);
 
+/* A render stream for lrt_render_device(_ex) that leaves the last `reserved_cus` CUs of the
+ * device free (hipExtStreamCreateWithCUMask), so that work on other streams -- the RCCL
+ * gather of the previous frame -- can run beside the persistent render kernel instead of
+ * waiting for its workgroups to retire; renders on it size their grid to the remaining
+ * CUs. Destroy with lrt_stream_destroy (lrt_shutdown destroys any left). */
+int lrt_stream_create(int reserved_cus, void** stream);
+int lrt_stream_destroy(void* stream);
+
 /* Number of local rows GPU `phase` owns in a row-block-cyclic split of `height` rows
  * into blocks of row_block rows dealt over `period` GPUs. */
 int lrt_shard_rows(int height, int row_block, int period, int phase);

@@ -359,6 +359,8 @@ struct Context {
     bool ready = false;
     int device = 0;
     int num_cus = 0;
+    // render streams created by lrt_stream_create: CU-masked, and the CUs they may use
+    std::vector<std::pair<hipStream_t, int>> masked_streams;
     unsigned int* d_queue = nullptr;   // kQueueSlots work counters, one per in-flight launch
     unsigned queue_next = 0;
     unsigned long long* d_tiles = nullptr;   // kQueueSlots x v0 counter sets (trace_kernel)
@@ -728,7 +730,12 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     hipError_t e = occupancy(&per_cu, kern, kBlock, ldsb);
     if (e != hipSuccess) return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
     if (per_cu < 1) return fail(LRT_E_INVALID, "trace_kernel does not fit on a CU");
-    long long blocks = (long long)per_cu * g_ctx.num_cus * LRT_V0_GRID_MULT;
+    // a CU-masked render stream (lrt_stream_create) gets a grid for the CUs it may use:
+    // persistent blocks beyond those would only start when others finish
+    int cus = g_ctx.num_cus;
+    for (const auto& m : g_ctx.masked_streams)
+        if (m.first == s) cus = m.second;
+    long long blocks = (long long)per_cu * cus * LRT_V0_GRID_MULT;
     if (blocks > ntiles) blocks = ntiles;
     const dim3 grid((unsigned)blocks);
     a.ovf = nullptr;
@@ -1115,6 +1122,7 @@ int lrt_shutdown(void) {
     g_ctx.d_tiles = nullptr;
     for (auto* f : g_ctx.d_feat)
         if (f) (void)hipFree(f);
+    for (auto& m : g_ctx.masked_streams) (void)hipStreamDestroy(m.first);
     if (g_ctx.stream) (void)hipStreamDestroy(g_ctx.stream);
     g_ctx = Context();
     return LRT_OK;
@@ -1190,6 +1198,43 @@ int lrt_render_host_ex(const lrt_render_desc* desc, float* backbuffer, long long
 int lrt_render_host(const lrt_render_desc* desc, float* backbuffer, long long* out_rays) {
     std::lock_guard<std::mutex> lk(g_mu);
     return render_host(desc, backbuffer, out_rays);
+}
+
+int lrt_stream_create(int reserved_cus, void** out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_ctx.ready) return fail(LRT_E_STATE, "lrt_initialize() has not been called");
+    if (!out) return fail(LRT_E_INVALID, "stream out is NULL");
+    const int n = g_ctx.num_cus;
+    if (reserved_cus < 0 || reserved_cus >= n) return fail(LRT_E_INVALID, "reserved_cus must be in [0, CU count)");
+    // the last reserved_cus logical CUs stay free; hipExtStreamCreateWithCUMask takes one
+    // bit per CU, 32 per word
+    std::vector<uint32_t> mask((size_t)(n + 31) / 32, 0u);
+    // Logical CU c sits on XCD c % 8 (measured: reserving CUs 31, 63, ... -- all on one XCD
+    // -- slows a full-chip render 20-70 %, because workgroups are dealt to XCDs round-robin),
+    // so the last reserved_cus logical CUs spread the reservation evenly over the XCDs.
+    int kept = 0;
+    for (int c = 0; c < n - reserved_cus; ++c) {
+        mask[c / 32] |= 1u << (c % 32);
+        ++kept;
+    }
+    hipStream_t st = nullptr;
+    LRT_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+    g_ctx.masked_streams.emplace_back(st, kept);
+    *out = st;
+    return LRT_OK;
+}
+
+int lrt_stream_destroy(void* stream) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto& v = g_ctx.masked_streams;
+    for (size_t i = 0; i < v.size(); ++i)
+        if (v[i].first == (hipStream_t)stream) {
+            (void)hipStreamSynchronize(v[i].first);
+            LRT_HIP(hipStreamDestroy(v[i].first));
+            v.erase(v.begin() + (long)i);
+            return LRT_OK;
+        }
+    return fail(LRT_E_INVALID, "not a stream from lrt_stream_create");
 }
 
 int lrt_shard_rows(int height, int row_block, int period, int phase) {

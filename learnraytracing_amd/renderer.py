@@ -164,6 +164,24 @@ def render_tensor(job: Job, buf, rays, stream=None) -> None:
                                       ctypes.c_void_p(rays.data_ptr()), ctypes.c_void_p(s.cuda_stream)))
 
 
+class RenderStream:
+    """A CU-masked render stream (lrt_stream_create) leaving `reserved_cus` CUs free for
+    concurrent work such as RCCL collectives; `.torch` is the torch.cuda.ExternalStream."""
+
+    def __init__(self, reserved_cus: int):
+        import torch
+
+        h = ctypes.c_void_p()
+        L.check(L.lib().lrt_stream_create(int(reserved_cus), ctypes.byref(h)))
+        self.handle = h.value
+        self.torch = torch.cuda.ExternalStream(self.handle)
+
+    def close(self) -> None:
+        if self.handle:
+            L.check(L.lib().lrt_stream_destroy(ctypes.c_void_p(self.handle)))
+            self.handle = None
+
+
 def unshard_tensor(gathered, out, width: int, height: int, row_block: int, period: int, stream=None) -> None:
     """Frame assembly (lrt_unshard_rows) on cuda tensors."""
     import torch

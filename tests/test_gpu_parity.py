@@ -270,3 +270,23 @@ def test_work_counters_across_slots_and_streams(gpu):
     for b, r in zip(bufs, rays):
         assert int(r.item()) == r1
         assert np.array_equal(b.cpu().numpy().view(np.uint32), one.view(np.uint32))
+
+
+def test_cu_reserved_render_stream(gpu):
+    """lrt_stream_create: a CU-masked stream (for overlap with RCCL) renders the same bits
+    with a grid sized to the CUs it may use."""
+    import torch
+    from learnraytracing_amd.renderer import RenderStream
+    want, wr = _render(gpu, 320, 180, 4, 8)
+    job = gpu.Job(width=320, height=180, frame0=0, frames=4, max_depth=8)
+    for reserved in (8, 200):
+        rs = RenderStream(reserved)
+        try:
+            buf = torch.zeros((180, 320, 4), dtype=torch.float32, device="cuda")
+            rays = torch.zeros(1, dtype=torch.int64, device="cuda")
+            gpu.render_tensor(job, buf, rays, rs.torch)
+            rs.torch.synchronize()
+            assert int(rays.item()) == wr
+            assert np.array_equal(buf.cpu().numpy().view(np.uint32), want.view(np.uint32))
+        finally:
+            rs.close()
