@@ -5,7 +5,8 @@
  * blit (main.cpp:117-141, removed), optionally writes the last frame as a PPM after
  * the same LinearToSRGB conversion.
  *
- *   lrt_demo [width height frames [out.ppm]]      defaults: 1280 720 16
+ *   lrt_demo [width height frames [out.ppm|out.pfm]]      defaults: 1280 720 16
+ * (.pfm: the linear float RGB backbuffer; otherwise sRGB 8-bit PPM)
  */
 #define _POSIX_C_SOURCE 199309L
 #include <math.h>
@@ -38,7 +39,7 @@ int main(int argc, char** argv) {
     int frames = argc > 3 ? atoi(argv[3]) : 16;
     const char* ppm = argc > 4 ? argv[4] : NULL;
     if (w < 1 || h < 1 || frames < 1) {
-        fprintf(stderr, "usage: %s [width height frames [out.ppm]]\n", argv[0]);
+        fprintf(stderr, "usage: %s [width height frames [out.ppm|out.pfm]]\n", argv[0]);
         return 2;
     }
     float* backbuffer = (float*)calloc((size_t)w * h * 4, sizeof(float)); /* main.cpp:40-41 */
@@ -63,7 +64,15 @@ int main(int argc, char** argv) {
     /* main.cpp:188-189 */
     printf("%.2fms (%.1f FPS) %.1fMrays/s %.2fMrays/frame frames %i\n", s * 1000.0, 1.0 / s,
            (double)total_rays / frames / s * 1.0e-6, (double)total_rays / frames * 1.0e-6, frames);
-    if (ppm) {
+    const size_t plen = ppm ? strlen(ppm) : 0;
+    if (ppm && plen > 4 && strcmp(ppm + plen - 4, ".pfm") == 0) {
+        /* linear float RGB; PFM stores rows bottom-to-top, the backbuffer's order */
+        FILE* fp = fopen(ppm, "wb");
+        if (!fp) return 1;
+        fprintf(fp, "PF\n%d %d\n-1.0\n", w, h);   /* negative scale: little-endian */
+        for (size_t i = 0; i < (size_t)w * h; ++i) fwrite(backbuffer + 4 * i, sizeof(float), 3, fp);
+        fclose(fp);
+    } else if (ppm) {
         FILE* fp = fopen(ppm, "wb");
         if (!fp) return 1;
         fprintf(fp, "P6\n%d %d\n255\n", w, h);
