@@ -113,6 +113,10 @@ typedef struct lrt_render_desc {
 #define LRT_F_V2 16          /* v2 persistent mode (work queue: static chunks, then
                                 atomics). With none of SIMPLE/V1/V2S/V2 set the library
                                 runs SIMPLE (fastest on every measured config).        */
+#define LRT_F_V3 128         /* v3 kernel: the v0 loop with path regeneration inside the
+                                wave (a lane traces its pixel's frames in turn; ended
+                                lanes are refilled together from the wave's pixel
+                                stream). No lrt_features.                              */
 
 /* ---- the reference API (parallel.h:6-8) ---------------------------------- */
 

@@ -73,6 +73,7 @@ struct KernelArgs {
     // world_pos_std (any may be null) and the last frame they are updated for (< 0: all)
     float4* feat[6];
     int featMax;
+    int regenMin;                 // v3: ended lanes that trigger a regeneration round
 };
 
 // AdaptiveStdvar (fragmentShader.fs.glsl:494-497) per channel, pow(x, 2) as x * x.
@@ -295,6 +296,10 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
     }
 #endif
 }
+
+}  // namespace lrt
+#include "lrt_regen.h"
+namespace lrt {
 
 // After a v0 launch (same stream): fold the per-queue ray counts into *rays and zero
 // the launch's counters for the slot's next use.
@@ -687,6 +692,34 @@ void wavetrace_dump(unsigned long long* d, size_t waves, hipStream_t s) {
 }
 #endif
 
+#ifdef LRT_EXP_SECSTATS
+unsigned long long* secstats_buffer(hipStream_t s) {
+    static unsigned long long* d_sec = nullptr;
+    if (!d_sec) (void)hipMalloc(&d_sec, sizeof(unsigned long long) * 3 * kSecN * 16);
+    (void)hipMemsetAsync(d_sec, 0, sizeof(unsigned long long) * 3 * kSecN * 16, s);
+    return d_sec;
+}
+void secstats_dump(const unsigned long long* d_sec, hipStream_t s) {
+        unsigned long long h[3 * kSecN * 16];
+        (void)hipMemcpyAsync(h, d_sec, sizeof(h), hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        const char* names[kSecN] = {"hit", "lambert", "shadow", "metal", "dielectric", "post", "fold", "camera", "other"};
+        double tot = 0;
+        for (int k = 0; k < kSecN; ++k)
+            for (int j = 0; j < 16; ++j) tot += (double)h[3 * (k + kSecN * j) + 2];
+        for (int k = 0; k < kSecN; ++k) {
+            unsigned long long ex = 0, ln = 0, cy = 0;
+            for (int j = 0; j < 16; ++j) {
+                ex += h[3 * (k + kSecN * j)];
+                ln += h[3 * (k + kSecN * j) + 1];
+                cy += h[3 * (k + kSecN * j) + 2];
+            }
+            fprintf(stderr, "secstats %-10s wave-execs %12llu  lanes/exec %6.2f  cycles %5.1f%%  cyc/exec %8.1f\n", names[k], ex,
+                    ex ? (double)ln / ex : 0.0, 100.0 * cy / tot, ex ? (double)cy / ex : 0.0);
+        }
+}
+#endif
+
 #ifndef LRT_V0_GRID_MULT
 #define LRT_V0_GRID_MULT 1
 #endif
@@ -741,9 +774,7 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     a.ovf = nullptr;
     a.tiles = g_ctx.d_tiles + (size_t)(g_ctx.tiles_next++ % kQueueSlots) * kTileSetU64;
 #ifdef LRT_EXP_SECSTATS
-    static unsigned long long* d_sec = nullptr;
-    if (!d_sec) (void)hipMalloc(&d_sec, sizeof(unsigned long long) * 3 * kSecN * 16);
-    (void)hipMemsetAsync(d_sec, 0, sizeof(unsigned long long) * 3 * kSecN * 16, s);
+    unsigned long long* d_sec = secstats_buffer(s);
     a.wtrace = d_sec;
 #endif
 #ifdef LRT_EXP_WAVETRACE
@@ -774,25 +805,7 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     wavetrace_dump(a.wtrace, (size_t)grid.x * (kBlock / 64), s);
 #endif
 #ifdef LRT_EXP_SECSTATS
-    {
-        unsigned long long h[3 * kSecN * 16];
-        (void)hipMemcpyAsync(h, d_sec, sizeof(h), hipMemcpyDeviceToHost, s);
-        (void)hipStreamSynchronize(s);
-        const char* names[kSecN] = {"hit", "lambert", "shadow", "metal", "dielectric", "post", "fold", "camera", "other"};
-        double tot = 0;
-        for (int k = 0; k < kSecN; ++k)
-            for (int j = 0; j < 16; ++j) tot += (double)h[3 * (k + kSecN * j) + 2];
-        for (int k = 0; k < kSecN; ++k) {
-            unsigned long long ex = 0, ln = 0, cy = 0;
-            for (int j = 0; j < 16; ++j) {
-                ex += h[3 * (k + kSecN * j)];
-                ln += h[3 * (k + kSecN * j) + 1];
-                cy += h[3 * (k + kSecN * j) + 2];
-            }
-            fprintf(stderr, "secstats %-10s wave-execs %12llu  lanes/exec %6.2f  cycles %5.1f%%  cyc/exec %8.1f\n", names[k], ex,
-                    ex ? (double)ln / ex : 0.0, 100.0 * cy / tot, ex ? (double)cy / ex : 0.0);
-        }
-    }
+    secstats_dump(d_sec, s);
 #endif
     if (a.ovf) {
         e = hipFreeAsync(a.ovf, s);
@@ -808,6 +821,77 @@ int launch_split(const KernelArgs& a, bool lds, int xc, int rows, int frames, bo
     if (LRT_MAX_SPLIT >= 4 && frames >= 4) return launch_depth<MAXD, (LRT_MAX_SPLIT >= 4 ? 4 : 1)>(a, lds, xc, rows, s);
     if (LRT_MAX_SPLIT >= 2 && frames >= 2) return launch_depth<MAXD, (LRT_MAX_SPLIT >= 2 ? 2 : 1)>(a, lds, xc, rows, s);
     return launch_depth<MAXD, 1>(a, lds, xc, rows, s);
+}
+
+// v3 (lrt_regen.h): same LDS layout, queues, counters and overflow stack as v0.
+template <int MAXD, int kSplit>
+int launch_regen(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
+    constexpr int kTileRows = 8 / kSplit;
+    const long long ntiles = (long long)((xc + 7) / 8) * ((rows + kTileRows - 1) / kTileRows);
+    const size_t stack = sizeof(float4) * kTraceLdsLevels * 64 + kPowTableBytes;
+    const size_t scene = lds ? sizeof(float4) * (4 * (size_t)a.count + (size_t)(a.nlights + 3) / 4 + 1) : 0;
+    a.bvh_stack_offset = (int)(stack + scene);
+    const size_t bstk = a.bv.on ? sizeof(unsigned short) * g_ctx.bvh_stack_levels * 64 : 0;
+    const size_t ldsb = stack + scene + bstk;
+    const void* kern = a.bv.on ? (lds ? (const void*)regen_kernel<MAXD, true, true, kSplit> : (const void*)regen_kernel<MAXD, false, true, kSplit>)
+                               : (lds ? (const void*)regen_kernel<MAXD, true, false, kSplit> : (const void*)regen_kernel<MAXD, false, false, kSplit>);
+    int per_cu = 0;
+    hipError_t e = occupancy(&per_cu, kern, 64, ldsb);
+    if (e != hipSuccess) return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
+    if (per_cu < 1) return fail(LRT_E_INVALID, "regen_kernel does not fit on a CU");
+    int cus = g_ctx.num_cus;
+    for (const auto& m : g_ctx.masked_streams)
+        if (m.first == s) cus = m.second;
+    long long blocks = (long long)per_cu * cus;
+    if (blocks > ntiles) blocks = ntiles;
+    const dim3 grid((unsigned)blocks);
+    a.ovf = nullptr;
+    a.tiles = g_ctx.d_tiles + (size_t)(g_ctx.tiles_next++ % kQueueSlots) * kTileSetU64;
+    if (a.regenMin <= 0) {
+        static int env = -1;
+        if (env < 0) {
+            const char* v = getenv("LRT_V3_REGEN_MIN");
+            env = v ? atoi(v) : 0;
+            if (env <= 0 || env > 64) env = 16;
+        }
+        a.regenMin = env;
+    }
+    if (a.maxDepth > kTraceLdsLevels) {
+        const size_t gthreads = (size_t)grid.x * 64;
+        e = hipMallocAsync((void**)&a.ovf, sizeof(float4) * gthreads * (size_t)(a.maxDepth - kTraceLdsLevels), s);
+        if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(trace stack overflow)");
+    }
+#ifdef LRT_EXP_SECSTATS
+    unsigned long long* d_sec = secstats_buffer(s);
+    a.wtrace = d_sec;
+#endif
+    if (a.bv.on) {
+        if (lds) regen_kernel<MAXD, true, true, kSplit><<<grid, 64, ldsb, s>>>(a);
+        else regen_kernel<MAXD, false, true, kSplit><<<grid, 64, ldsb, s>>>(a);
+    } else {
+        if (lds) regen_kernel<MAXD, true, false, kSplit><<<grid, 64, ldsb, s>>>(a);
+        else regen_kernel<MAXD, false, false, kSplit><<<grid, 64, ldsb, s>>>(a);
+    }
+    e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "regen_kernel launch");
+    rays_collect_kernel<<<1, 64, 0, s>>>(a.tiles, a.rays);
+    e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "rays_collect_kernel launch");
+#ifdef LRT_EXP_SECSTATS
+    secstats_dump(d_sec, s);
+#endif
+    if (a.ovf) {
+        e = hipFreeAsync(a.ovf, s);
+        if (e != hipSuccess) return hip_fail(e, "hipFreeAsync(trace stack overflow)");
+    }
+    return LRT_OK;
+}
+
+template <int MAXD>
+int launch_regen_split(const KernelArgs& a, bool lds, int xc, int rows, int frames, hipStream_t s) {
+    if (frames >= 4) return launch_regen<MAXD, 4>(a, lds, xc, rows, s);
+    if (frames >= 2) return launch_regen<MAXD, 2>(a, lds, xc, rows, s);
+    return launch_regen<MAXD, 1>(a, lds, xc, rows, s);
 }
 
 template <bool kLdsScene, bool kV2, bool kOverflow, int kPix = 0, bool kBvh = false>
@@ -935,10 +1019,18 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     // blocks on spread tile queues, 4 waves/SIMD -- is fastest on every BASELINE config
     // (config 2: 0.46 vs 0.64 ms, config 3: 4.15 vs 4.32 ms, config 4: 538 vs 575 ms
     // for v2s); v1/v2/v2s stay selectable for A/B.
-    int kflags = d->flags & (LRT_F_SIMPLE | LRT_F_V1 | LRT_F_V2S | LRT_F_V2);
+    a.regenMin = 0;
+    int kflags = d->flags & (LRT_F_SIMPLE | LRT_F_V1 | LRT_F_V2S | LRT_F_V2 | LRT_F_V3);
     if (kflags == 0) kflags = LRT_F_SIMPLE;
-    if ((a.ndl || want_feat) && !(kflags & LRT_F_SIMPLE))
-        return fail(LRT_E_INVALID, "LRT_F_NO_DOUBLE_LIGHT and features are implemented by the v0 kernel only");
+    if (want_feat && !(kflags & LRT_F_SIMPLE))
+        return fail(LRT_E_INVALID, "features are implemented by the v0 kernel only");
+    if (a.ndl && !(kflags & (LRT_F_SIMPLE | LRT_F_V3)))
+        return fail(LRT_E_INVALID, "LRT_F_NO_DOUBLE_LIGHT is implemented by the v0 and v3 kernels only");
+    if (kflags & LRT_F_V3) {
+        if (d->max_depth <= 8) return launch_regen_split<8>(a, lds, d->x_count, d->row_count, d->frames, s);
+        if (d->max_depth <= 20) return launch_regen_split<20>(a, lds, d->x_count, d->row_count, d->frames, s);
+        return launch_regen_split<64>(a, lds, d->x_count, d->row_count, d->frames, s);
+    }
     if (!(kflags & LRT_F_SIMPLE)) {
         PathArgs p;
         p.cam = a.cam;

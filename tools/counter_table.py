@@ -7,7 +7,7 @@ for f in sorted(glob.glob(os.path.join(d, "*_g*_counter_collection.csv"))):
     k = os.path.basename(f).split("_g")[0]
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
-        if "paths" in r["Kernel_Name"] or "trace_kernel" in r["Kernel_Name"]:
+        if any(s in r["Kernel_Name"] for s in ("paths", "trace_kernel", "regen_kernel")):
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
     for c, v in agg.items():
         table[c][k] = sum(v) / len(v)
