@@ -68,7 +68,7 @@ LRT_DEV int ClosestHitBVH(const F3& o, const F3& d, const BvhView& bv, float& tO
             const float rsProj = dot(rs, d);
             const float ifHit = dot(rs, rs) - rsProj * rsProj - s.w;
             if (ifHit < 0.0f) {
-                const float halfCut = __builtin_sqrtf(-ifHit);
+                const float halfCut = sqrt_rn(-ifHit);
                 const float t1 = rsProj - halfCut;
                 const float t2 = rsProj + halfCut;
                 const float cand = t1 > kMinT ? t1 : (t2 > kMinT ? t2 : __builtin_inff());
@@ -131,7 +131,7 @@ LRT_DEV float SphereCand(const F3& o, const F3& d, const float4& s) {   // maths
     const float rsProj = dot(rs, d);
     const float ifHit = dot(rs, rs) - rsProj * rsProj - s.w;
     if (!(ifHit < 0.0f)) return __builtin_inff();
-    const float halfCut = __builtin_sqrtf(-ifHit);
+    const float halfCut = sqrt_rn(-ifHit);
     const float t1 = rsProj - halfCut;
     const float t2 = rsProj + halfCut;
     return t1 > kMinT ? t1 : (t2 > kMinT ? t2 : __builtin_inff());

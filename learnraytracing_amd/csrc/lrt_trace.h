@@ -37,15 +37,62 @@ LRT_DEV float dot(F3 a, F3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }     
 LRT_DEV F3 cross(F3 a, F3 b) {                                                      // maths.h:87-92
     return f3(a.y * b.z - a.z * b.y, -(a.x * b.z - a.z * b.x), a.x * b.y - a.y * b.x);
 }
-LRT_DEV float length(F3 v) { return __builtin_sqrtf(v.x * v.x + v.y * v.y + v.z * v.z); } // maths.h:15
-LRT_DEV F3 normalize(F3 v) { float k = 1.0f / length(v); return f3(v.x * k, v.y * k, v.z * k); } // maths.h:93
+// Correctly rounded sqrt and reciprocal (the IEEE results the reference's sqrtf and 1/x
+// give) in fewer instructions than LLVM's generic expansions, which also handle operands
+// the path almost never produces:
+//  * sqrt: v_sqrt_f32 is faithful (within 1 ulp); one residual check of each neighbour,
+//    fma(-s', s, x), picks the correctly rounded root. This is LLVM's own sequence minus
+//    the denormal scaling and the 0/inf class fix-up, and equals __builtin_sqrtf for
+//    every float >= 2^-104 (checked exhaustively on gfx950: tools/fpexact.hip).
+//  * reciprocal: v_rcp_f32 plus two Newton steps in fma, equal to 1.0f / x for every
+//    float with |x| in [2^-125, 2^125] (exhaustive, tools/fpexact.hip).
+// Operands outside those ranges (or NaN) send the whole wave through the generic
+// sequence: a wave-uniform branch, essentially never taken. Host builds (the BVH
+// diagnostics) use the plain operations.
+#ifndef LRT_FAST_SQRT
+#define LRT_FAST_SQRT 1
+#endif
+#ifndef LRT_FAST_RCP
+#define LRT_FAST_RCP 1
+#endif
+LRT_DEV float sqrt_rn(float x) {
+#if LRT_FAST_SQRT && defined(__HIP_DEVICE_COMPILE__)
+    float s = __builtin_amdgcn_sqrtf(x);
+    const float sd = __int_as_float(__float_as_int(s) - 1);
+    const float su = __int_as_float(__float_as_int(s) + 1);
+    const float rd = __builtin_fmaf(-sd, s, x);
+    const float ru = __builtin_fmaf(-su, s, x);
+    s = rd <= 0.0f ? sd : s;
+    s = ru > 0.0f ? su : s;
+    if (__builtin_expect(__ballot(!(x >= 0x1p-96f)) != 0, 0)) s = __builtin_sqrtf(x);
+    return s;
+#else
+    return __builtin_sqrtf(x);
+#endif
+}
+LRT_DEV float rcp_rn(float x) {
+#if LRT_FAST_RCP && defined(__HIP_DEVICE_COMPILE__)
+    float r = __builtin_amdgcn_rcpf(x);
+    float e = __builtin_fmaf(-x, r, 1.0f);
+    r = __builtin_fmaf(e, r, r);
+    e = __builtin_fmaf(-x, r, 1.0f);
+    r = __builtin_fmaf(e, r, r);
+    const float ax = __builtin_fabsf(x);
+    if (__builtin_expect(__ballot(!(ax >= 0x1p-125f && ax <= 0x1p125f)) != 0, 0)) r = 1.0f / x;
+    return r;
+#else
+    return 1.0f / x;
+#endif
+}
+LRT_DEV float length(F3 v) { return sqrt_rn(v.x * v.x + v.y * v.y + v.z * v.z); } // maths.h:15
+LRT_DEV F3 normalize(F3 v) { float k = rcp_rn(length(v)); return f3(v.x * k, v.y * k, v.z * k); } // maths.h:93
 LRT_DEV F3 normalize_member(F3 v) { float l = length(v); return f3(v.x / l, v.y / l, v.z / l); } // maths.h:19
 LRT_DEV F3 reflect(F3 v, F3 n) { return v + 2.0f * (-dot(v, n) * n); }             // maths.h:100-103
 LRT_DEV bool refract(F3 v, F3 n, float nint, F3& out) {                             // maths.h:106-118
     float dt = dot(v, n);
     float discr = 1.0f - nint * nint * (1.0f - dt * dt);
     if (discr > 0) {
-        out = nint * (v - n * dt) - n * __builtin_sqrtf(discr);
+        out = nint * (v - n * dt) - n * sqrt_rn(discr);
         return true;
     }
     return false;
@@ -87,7 +134,7 @@ LRT_DEV F3 RandomInUnitDisk(uint32_t& s) {
 LRT_DEV F3 RandomUnitVector(uint32_t& s) {
     float z = RandomFloat01(s) * 2.0f - 1.0f;
     float a = RandomFloat01(s) * 2.0f * kPI;
-    float r = __builtin_sqrtf(1.0f - z * z);
+    float r = sqrt_rn(1.0f - z * z);
     float sa, ca;
     libm::sincosf(a, &sa, &ca);   // bit-identical to separate cosf(a), sinf(a)
     float x = r * ca;
@@ -197,6 +244,41 @@ LRT_DEV void sec_enter(const SceneView& sc, int sec, bool count) {
 }
 LRT_DEV void sec_count(const SceneView& sc, int sec) { sec_enter(sc, sec, true); }
 
+// HitSphere's root selection against the running closestT (maths.cpp:61-90): the first
+// root if it lies in (tMin, closestT), else the second. LRT_BRANCHLESS_HIT evaluates it
+// with selects for every lane (sqrt of a dummy 1 where the ray misses) instead of a
+// divergent branch around the sqrt; same values either way.
+#ifndef LRT_BRANCHLESS_HIT
+#define LRT_BRANCHLESS_HIT 0
+#endif
+LRT_DEV void SphereRoots(float rsProj, float ifHit, float tMin, float& closestT, int& id, int i) {
+#if LRT_BRANCHLESS_HIT
+    const bool h = ifHit < 0.0f;
+    const float halfCut = sqrt_rn(h ? -ifHit : 1.0f);
+    const float t1 = rsProj - halfCut;
+    const float t2 = rsProj + halfCut;
+    const bool c1 = h && t1 > tMin && t1 < closestT;
+    const bool c2 = h && !c1 && t2 > tMin && t2 < closestT;
+    closestT = c1 ? t1 : (c2 ? t2 : closestT);
+    id = (c1 || c2) ? i : id;
+#else
+    if (ifHit < 0.0f) {
+        const float halfCut = sqrt_rn(-ifHit);
+        float t = rsProj - halfCut;
+        if (t > tMin && t < closestT) {
+            closestT = t;
+            id = i;
+        } else {
+            t = rsProj + halfCut;
+            if (t > tMin && t < closestT) {
+                closestT = t;
+                id = i;
+            }
+        }
+    }
+#endif
+}
+
 // HitWorld + HitSphere (parallel.cpp:54-73, maths.cpp:51-94). The per-sphere test
 // is the reference's; hit position and normal are computed once for the winner
 // (they are pure functions of (ray, t, sphere), so this is bit-identical to the
@@ -215,20 +297,7 @@ LRT_DEV int ClosestHitSV(const Ray& r, float tMin, float tMax, const SceneView& 
         F3 rs = f3(s.x, s.y, s.z) - r.orig;
         float rsProj = dot(rs, r.dir);
         float ifHit = dot(rs, rs) - rsProj * rsProj - s.w;
-        if (ifHit < 0.0f) {
-            float halfCut = __builtin_sqrtf(-ifHit);
-            float t = rsProj - halfCut;
-            if (t > tMin && t < closestT) {
-                closestT = t;
-                id = i;
-            } else {
-                t = rsProj + halfCut;
-                if (t > tMin && t < closestT) {
-                    closestT = t;
-                    id = i;
-                }
-            }
-        }
+        SphereRoots(rsProj, ifHit, tMin, closestT, id, i);
     }
     tOut = closestT;
     return id;
@@ -282,15 +351,15 @@ LRT_DEV F3 ScatterDir(const Material& mat, int matId, const Ray& r_in, const Hit
             // -(c - pos) exactly, so both lengths are the same float -- computed once
             const F3 cp = c - rec.pos;
             const float len = length(cp);
-            const float kinv = 1.0f / len;
+            const float kinv = rcp_rn(len);
             F3 sw = f3(cp.x * kinv, cp.y * kinv, cp.z * kinv);
             F3 su = normalize(cross(__builtin_fabsf(sw.x) > 0.01f ? f3(0.0f, 1.0f, 0.0f) : f3(1.0f, 0.0f, 0.0f), sw));
             F3 sv = cross(sw, su);
-            float cosAMax = __builtin_sqrtf(1.0f - s.w / (len * len));                    // :109
+            float cosAMax = sqrt_rn(1.0f - s.w / (len * len));                    // :109
             float eps1 = RandomFloat01(rng);
             float eps2 = RandomFloat01(rng);
             float cosA = 1.0f - eps1 + eps1 * cosAMax;
-            float sinA = __builtin_sqrtf(1.0f - cosA * cosA);
+            float sinA = sqrt_rn(1.0f - cosA * cosA);
             float phi = 2.0f * kPI * eps2;
             float sphi, cphi;
             libm::sincosf(phi, &sphi, &cphi);   // bit-identical to cosf(phi), sinf(phi)
@@ -351,7 +420,7 @@ LRT_DEV F3 ScatterDir(const Material& mat, int matId, const Ray& r_in, const Hit
         cosine = dot(rdir, rec.normal);
     } else {
         outwardN = rec.normal;
-        nint = 1.0f / mat.ri;
+        nint = rcp_rn(mat.ri);
         cosine = -dot(rdir, rec.normal);
     }
     if (refract(rdir, outwardN, nint, refr))
@@ -464,38 +533,12 @@ LRT_DEV void DualClosestHit(const F3& o, const F3& db, bool hasShadow, const F3&
         {
             const float rsProj = dot(rs, db);
             const float ifHit = rr - rsProj * rsProj - s.w;
-            if (ifHit < 0.0f) {
-                const float halfCut = __builtin_sqrtf(-ifHit);
-                float t = rsProj - halfCut;
-                if (t > kMinT && t < closestB) {
-                    closestB = t;
-                    idB = i;
-                } else {
-                    t = rsProj + halfCut;
-                    if (t > kMinT && t < closestB) {
-                        closestB = t;
-                        idB = i;
-                    }
-                }
-            }
+            SphereRoots(rsProj, ifHit, kMinT, closestB, idB, i);
         }
         if (hasShadow) {
             const float rsProj = dot(rs, ds);
             const float ifHit = rr - rsProj * rsProj - s.w;
-            if (ifHit < 0.0f) {
-                const float halfCut = __builtin_sqrtf(-ifHit);
-                float t = rsProj - halfCut;
-                if (t > kMinT && t < closestS) {
-                    closestS = t;
-                    idS = i;
-                } else {
-                    t = rsProj + halfCut;
-                    if (t > kMinT && t < closestS) {
-                        closestS = t;
-                        idS = i;
-                    }
-                }
-            }
+            SphereRoots(rsProj, ifHit, kMinT, closestS, idS, i);
         }
     }
     tB = closestB;

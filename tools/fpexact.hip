@@ -9,6 +9,8 @@
 #include <stdint.h>
 #include <stdio.h>
 
+#include "../learnraytracing_amd/csrc/lrt_trace.h"   // the product's sqrt_rn / rcp_rn
+
 __device__ __forceinline__ float sqrt_fix(float x) {   // v_sqrt + two-sided 1-ulp correction
     float s = __builtin_amdgcn_sqrtf(x);
     float sd = __int_as_float(__float_as_int(s) - 1);
@@ -37,6 +39,26 @@ __device__ __forceinline__ float div_mk2(float a, float b) {   // two correction
     q = __builtin_fmaf(r, y, q);
     r = __builtin_fmaf(-b, q, a);
     return __builtin_fmaf(r, y, q);
+}
+
+__device__ __forceinline__ float rcp_nr2(float x) {   // v_rcp + two Newton steps
+    float r = __builtin_amdgcn_rcpf(x);
+    float e = __builtin_fmaf(-x, r, 1.0f);
+    r = __builtin_fmaf(e, r, r);
+    e = __builtin_fmaf(-x, r, 1.0f);
+    return __builtin_fmaf(e, r, r);
+}
+__device__ __forceinline__ bool same(float a, float b) {
+    return __float_as_uint(a) == __float_as_uint(b) || (a != a && b != b);
+}
+// the product functions over every 32-bit pattern (signs, zeros, denormals, inf, NaN)
+__global__ void prod_kernel(uint32_t base, unsigned long long* cnt) {
+    const uint32_t u = base + blockIdx.x * blockDim.x + threadIdx.x;
+    const float x = __uint_as_float(u);
+    if (!same(lrt::sqrt_rn(x), __builtin_sqrtf(x))) atomicAdd(&cnt[0], 1ull);
+    if (!same(lrt::rcp_rn(x), 1.0f / x)) atomicAdd(&cnt[1], 1ull);
+    const uint32_t a = u & 0x7fffffffu;
+    if (a >= 0x01000000u && a < 0x7f000000u && rcp_nr2(x) != 1.0f / x) atomicAdd(&cnt[2 + ((a >> 23) & 0xff)], 1ull);
 }
 
 // per biased exponent (0..255) mismatch counts for each unary test
@@ -102,6 +124,20 @@ int main() {
         for (int e = 0; e < 256; ++e)
             if (h[k * 256 + e] && (e < 40 || e > 215))
                 printf("    e=%3d: %llu\n", e, h[k * 256 + e]);
+    }
+    {
+        unsigned long long* c = d;
+        hipMemset(c, 0, (2 + 256) * 8);
+        for (uint64_t base = 0; base < 0x100000000ull; base += 1ull << 28)
+            prod_kernel<<<(1u << 28) / 256, 256>>>((uint32_t)base, c);
+        unsigned long long hc[2 + 256];
+        hipMemcpy(hc, c, sizeof(hc), hipMemcpyDeviceToHost);
+        printf("product sqrt_rn vs sqrtf over all 2^32 patterns: %llu mismatches\n", hc[0]);
+        printf("product rcp_rn vs 1/x over all 2^32 patterns: %llu mismatches\n", hc[1]);
+        unsigned long long t = 0;
+        int lo = -1, hi = -1;
+        for (int e = 0; e < 256; ++e) if (hc[2 + e]) { t += hc[2 + e]; if (lo < 0) lo = e; hi = e; }
+        printf("rcp_nr2 (|x| in [2^-126, 2^127)) mismatches %llu (biased exponents %d..%d)\n", t, lo, hi);
     }
     const int ranges[][2] = {{-20, 20}, {-60, 60}, {-1, 1}, {-126, 127}};
     for (auto& r : ranges) {
