@@ -137,6 +137,10 @@ def main():
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--row-block", type=int, default=8)
+    ap.add_argument("--spp", type=int, default=None, help="diagnostic: override the config's spp per GPU")
+    ap.add_argument("--shard-of", type=int, default=1,
+                    help="diagnostic (1 process): render only rank 0's shard of an N-GPU weak-scaling run, "
+                         "no gather -- the per-GPU render time at N GPUs, measured on one")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=None, help="seconds of CPU-baseline timing")
     ap.add_argument("--scene-global", action="store_true", help="read spheres from global memory, not LDS")
@@ -154,6 +158,8 @@ def main():
     if world != args.gpus:
         log(f"note: WORLD_SIZE={world} but --gpus {args.gpus}; using WORLD_SIZE")
     cfg = dict(CONFIGS[args.config])
+    if args.spp:
+        cfg["spp"] = args.spp
     cfg_name = f"config{args.config}"
 
     # CPU baseline first: rank 0 at N=1 only, before anything touches the GPU.
@@ -168,11 +174,13 @@ def main():
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local_rank if os.environ.get("LRT_DIST_BACKEND", "nccl") == "nccl" else 0)
     backend = os.environ.get("LRT_DIST_BACKEND", "nccl")   # nccl = RCCL; gloo only to rehearse on 1 GPU
+    # LRT_BENCH_SAME_GPU=1 puts every rank on GPU 0 (rehearsing the RCCL path on a 1-GPU box)
+    gpu = 0 if (backend != "nccl" or os.environ.get("LRT_BENCH_SAME_GPU") == "1") else local_rank
+    torch.cuda.set_device(gpu)
     if world > 1:
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
         else:
             dist.init_process_group(backend)
     import learnraytracing_amd as lrt
@@ -193,13 +201,14 @@ def main():
     if cfg["scene"] == "random1000":
         lrt.set_scene(*lrt.random_scene(1000, 1))
     W, H, D = cfg["width"], cfg["height"], cfg["depth"]
-    spp_total = cfg["spp"] * world if args.scaling == "weak" else cfg["spp"]
-    rb = H if world == 1 else args.row_block
-    max_rows = max_shard_rows(H, rb, world)
-    rows = shard_rows(H, rb, world, rank)
+    shards = world if world > 1 else max(1, args.shard_of)   # row shards of the frame
+    spp_total = cfg["spp"] * shards if args.scaling == "weak" else cfg["spp"]
+    rb = H if shards == 1 else args.row_block
+    max_rows = max_shard_rows(H, rb, shards)
+    rows = shard_rows(H, rb, shards, rank)
     flags = (1 if args.scene_global else 0) | {"auto": 0, "v0": 2, "v1": 4, "v2": 16, "v2s": 8, "v3": 128}[args.kernel]
     job = lrt.Job(width=W, height=H, frame0=0, frames=spp_total, max_depth=D, row_block=rb,
-                  row_period=world, row_phase=rank, row_count=rows, flags=flags)
+                  row_period=shards, row_phase=rank, row_count=rows, flags=flags)
     dev = torch.device("cuda", torch.cuda.current_device())
     bufs = [torch.zeros((max_rows, W, 4), dtype=torch.float32, device=dev) for _ in range(2)]
     rays = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -294,7 +303,8 @@ def main():
                 "width": W, "height": H, "spp_per_gpu": cfg["spp"], "spp_total": spp_total, "max_depth": D,
                 "rays_per_step": int(total_rays / args.steps),
                 "parallelism": f"rows: row-block-cyclic x{world} (block {rb}), RCCL gather to rank 0"
-                if world > 1 else "single GPU",
+                if world > 1 else ("single GPU" if shards == 1 else
+                                   f"DIAGNOSTIC: rank 0's shard of {shards} (block {rb}), no gather"),
                 "scene_reads": "global" if args.scene_global else "LDS-staged",
                 "reserved_cus": reserve,
                 "kernel": args.kernel,

@@ -213,7 +213,8 @@ int lrt_unshard_rows(const float* d_src, float* d_dst, int width, int height, in
 int lrt_present_bgra8(const float* d_rgba, uint32_t* d_bgra, int width, int height, void* stream);
 
 /* ---- diagnostics (libm restatement, lrt_libm.h) --------------------------- */
-/* kind 0: sinf, 1: cosf, 2: powf(x, 5), 3: powf(x, 0.416666667f) (LinearToSRGB).
+/* kind 0: sinf, 1: cosf, 2: powf(x, 5), 3: powf(x, 0.416666667f) (LinearToSRGB),
+ * 4: sqrtf, 5: 1.0f / x (the device evaluates the path's short correctly rounded sequences).
  * Host evaluation of the restatement. */
 int lrt_libm_eval_host(int kind, const float* in, float* out, long long n);
 /* Device evaluation of the same restatement (device pointers, blocking). */

@@ -37,7 +37,8 @@ constexpr int kBlock = LRT_V0_BLOCK;
 static_assert(kBlock == 64 || kBlock == 256, "v0 block: 1 or 4 waves");
 constexpr int kBlockWavesX = kBlock == 256 ? 2 : 1;           // waves per block in x
 constexpr int kBlockWavesY = kBlock / 64 / kBlockWavesX;       // and in y
-constexpr int kTileX = 8 * kBlockWavesX;                       // pixels per block in x
+// a wave's pixels: 64 / kSplit of them, 8 wide (kSplit <= 8) or a single row
+constexpr int WaveCols(int split) { return split <= 8 ? 8 : 64 / split; }
 #ifndef LRT_V0_DYNAMIC
 #define LRT_V0_DYNAMIC 1
 #endif
@@ -74,7 +75,9 @@ struct KernelArgs {
     float4* feat[6];
     int featMax;
     int regenMin;                 // v3: ended lanes that trigger a regeneration round
+    const float* lerp;            // lerpFac = (float)f / (float)(f + 1) for f < kLerpTable (parallel.cpp:262)
 };
+constexpr int kLerpTable = 1 << 16;
 
 // AdaptiveStdvar (fragmentShader.fs.glsl:494-497) per channel, pow(x, 2) as x * x.
 LRT_DEV float adaptive_std(float lastStd, float lastMean, int n, float newVal, float newMean) {
@@ -172,11 +175,13 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
     const size_t gtid = (size_t)blockIdx.x * kBlock + tid;
     const size_t gthreads = (size_t)gridDim.x * kBlock;
 
-    // wave = 8 x (8 / kSplit) pixels x kSplit frame lanes; block = kBlockWavesX x kBlockWavesY waves
+    // wave = kWaveCols x kWaveRows pixels x kSplit frame lanes; block = kBlockWavesX x kBlockWavesY waves
     const int wave = tid >> 6, lane = tid & 63;
     const int sub = lane % kSplit, p = lane / kSplit;
-    constexpr int kWaveRows = 8 / kSplit;
+    constexpr int kWaveCols = WaveCols(kSplit);
+    constexpr int kWaveRows = 64 / kSplit / kWaveCols;
     constexpr int kTileRows = kBlockWavesY * kWaveRows;
+    constexpr int kTileX = kWaveCols * kBlockWavesX;
     const int tilesX = (a.xc + kTileX - 1) / kTileX;
     const int ntiles = tilesX * ((a.rows + kTileRows - 1) / kTileRows);
     const float invWidth = 1.0f / (float)a.width;     // parallel.cpp:260
@@ -194,8 +199,8 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
         // the atomic would wait for it) and consumed after the trace, which hides it.
         // (Prefetching the next tile's pixels as well costs VGPRs beyond the 128 cap.)
         const int tile = q + kV0Queues * i;
-        const int lx = (tile % tilesX) * kTileX + (wave % kBlockWavesX) * 8 + (p & 7);
-        const int ly = (tile / tilesX) * kTileRows + (wave / kBlockWavesX) * kWaveRows + (p >> 3);
+        const int lx = (tile % tilesX) * kTileX + (wave % kBlockWavesX) * kWaveCols + (p % kWaveCols);
+        const int ly = (tile / tilesX) * kTileRows + (wave / kBlockWavesX) * kWaveRows + (p / kWaveCols);
         const bool valid = lx < a.xc && ly < a.rows;
         const int x = a.x0 + lx;
         const int y = valid ? a.y0 + (ly / a.rb) * a.rb * a.rp + a.rph * a.rb + ly % a.rb : 0;
@@ -223,13 +228,22 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
                 col = Trace<MAXD, kBvh, kFeat>(r, a.maxDepth, rays, rng, sc, smem + tid, kBlock, a.ovf + gtid,
                                                gthreads, a.ndl, feat);
             }
+            // the group's colours go through this lane's (now free) stack level 0 in LDS:
+            // one write, then one read per frame, instead of three shuffles per frame
+            if (kSplit > 1) {
+                smem[tid] = make_float4(col.x, col.y, col.z, 0.0f);
+                __builtin_amdgcn_wave_barrier();
+            }
 #pragma unroll
             for (int j = 0; j < kSplit; ++j) {
-                const int src = lane - sub + j;
-                F3 c = kSplit == 1 ? col : f3(__shfl(col.x, src, 64), __shfl(col.y, src, 64), __shfl(col.z, src, 64));
-                const int fj = f0 + j;
+                F3 c = col;
+                if (kSplit > 1) {
+                    const float4 cj = smem[tid - sub + j];
+                    c = f3(cj.x, cj.y, cj.z);
+                }
+                const int fj = f0 + j;   // wave-uniform: the factor is a scalar load
                 if (fj < fend) {
-                    const float lerpFac = (float)fj / (float)(fj + 1);             // :262
+                    const float lerpFac = fj < kLerpTable ? a.lerp[fj] : (float)fj / (float)(fj + 1);   // :262
                     const float4 last = acc;
                     F3 prev = f3(acc.x, acc.y, acc.z);
                     const F3 sample = c;
@@ -250,6 +264,7 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
                     }
                 }
             }
+            if (kSplit > 1) __builtin_amdgcn_wave_barrier();
         }
         if (valid && sub == 0) *px = acc;
         if constexpr (kFeat) {
@@ -343,8 +358,12 @@ __global__ void present_kernel(const float4* __restrict__ src, uint32_t* __restr
 }
 
 LRT_HD float libm_eval(int kind, float x) {
-    return kind == 0 ? libm::sinf(x) : kind == 1 ? libm::cosf(x) : kind == 2 ? libm::powf5(x)
-                                                                            : libm::powf(x, 0.416666667f);
+    return kind == 0   ? libm::sinf(x)
+           : kind == 1 ? libm::cosf(x)
+           : kind == 2 ? libm::powf5(x)
+           : kind == 3 ? libm::powf(x, 0.416666667f)
+           : kind == 4 ? sqrt_rn(x)    // the path's correctly rounded sqrt (fast sequence on the device)
+                       : rcp_rn(x);    // and reciprocal
 }
 
 __global__ void libm_kernel(int kind, const float* __restrict__ in, float* __restrict__ out, long long n) {
@@ -369,6 +388,7 @@ struct Context {
     unsigned int* d_queue = nullptr;   // kQueueSlots work counters, one per in-flight launch
     unsigned queue_next = 0;
     unsigned long long* d_tiles = nullptr;   // kQueueSlots x v0 counter sets (trace_kernel)
+    float* d_lerp = nullptr;                 // kLerpTable lerp factors (host IEEE division)
     unsigned tiles_next = 0;
     hipStream_t stream = nullptr;
     int count = 0, nlights = 0;
@@ -741,12 +761,13 @@ hipError_t occupancy(int* per_cu, const void* kern, int block, size_t lds) {
 }
 
 #ifndef LRT_MAX_SPLIT
-#define LRT_MAX_SPLIT 4
+#define LRT_MAX_SPLIT 16
 #endif
 
 template <int MAXD, int kSplit, bool kFeat = false>
 int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
-    constexpr int kTileRows = kBlockWavesY * (8 / kSplit);
+    constexpr int kTileRows = kBlockWavesY * (64 / kSplit / WaveCols(kSplit));
+    constexpr int kTileX = WaveCols(kSplit) * kBlockWavesX;
     const long long ntiles = (long long)((xc + kTileX - 1) / kTileX) * ((rows + kTileRows - 1) / kTileRows);
     const size_t stack = sizeof(float4) * kTraceLdsLevels * kBlock + kPowTableBytes;
     const size_t scene = lds ? sizeof(float4) * (4 * (size_t)a.count + (size_t)(a.nlights + 3) / 4 + 1) : 0;
@@ -817,10 +838,24 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
 template <int MAXD>
 int launch_split(const KernelArgs& a, bool lds, int xc, int rows, int frames, bool feat, hipStream_t s) {
     if (feat) return launch_depth<MAXD, 1, true>(a, lds, xc, rows, s);
-    // one lane per frame of a pixel, up to LRT_MAX_SPLIT lanes per pixel
-    if (LRT_MAX_SPLIT >= 4 && frames >= 4) return launch_depth<MAXD, (LRT_MAX_SPLIT >= 4 ? 4 : 1)>(a, lds, xc, rows, s);
-    if (LRT_MAX_SPLIT >= 2 && frames >= 2) return launch_depth<MAXD, (LRT_MAX_SPLIT >= 2 ? 2 : 1)>(a, lds, xc, rows, s);
-    return launch_depth<MAXD, 1>(a, lds, xc, rows, s);
+    // one lane per frame of a pixel: the largest power of two <= frames, up to
+    // LRT_MAX_SPLIT lanes per pixel. Fewer lanes per pixel than frames means several
+    // rounds per wave task, i.e. fewer, longer tasks: with few pixels (one GPU's row shard
+    // at 8 GPUs: 115,200 pixels at 32 spp) 7,200 tasks of 8 rounds on 4,096 waves left a
+    // 1.7x tail (0.635 ms vs 0.365 for the same rays). Each lane replays its group's lerp
+    // chain, so the merge costs kSplit steps per round: 16 measured best (shard of 8:
+    // 0.437 ms, 32 lanes: 0.446; config 4 at 64 spp: 457 ms, 64 lanes: 478).
+    int split = 1;
+    while (split * 2 <= frames && split * 2 <= LRT_MAX_SPLIT) split *= 2;
+    switch (split) {
+        case 64: return launch_depth<MAXD, (LRT_MAX_SPLIT >= 64 ? 64 : 1)>(a, lds, xc, rows, s);
+        case 32: return launch_depth<MAXD, (LRT_MAX_SPLIT >= 32 ? 32 : 1)>(a, lds, xc, rows, s);
+        case 16: return launch_depth<MAXD, (LRT_MAX_SPLIT >= 16 ? 16 : 1)>(a, lds, xc, rows, s);
+        case 8: return launch_depth<MAXD, (LRT_MAX_SPLIT >= 8 ? 8 : 1)>(a, lds, xc, rows, s);
+        case 4: return launch_depth<MAXD, (LRT_MAX_SPLIT >= 4 ? 4 : 1)>(a, lds, xc, rows, s);
+        case 2: return launch_depth<MAXD, (LRT_MAX_SPLIT >= 2 ? 2 : 1)>(a, lds, xc, rows, s);
+        default: return launch_depth<MAXD, 1>(a, lds, xc, rows, s);
+    }
 }
 
 // v3 (lrt_regen.h): same LDS layout, queues, counters and overflow stack as v0.
@@ -1020,6 +1055,7 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     // (config 2: 0.46 vs 0.64 ms, config 3: 4.15 vs 4.32 ms, config 4: 538 vs 575 ms
     // for v2s); v1/v2/v2s stay selectable for A/B.
     a.regenMin = 0;
+    a.lerp = g_ctx.d_lerp;
     int kflags = d->flags & (LRT_F_SIMPLE | LRT_F_V1 | LRT_F_V2S | LRT_F_V2 | LRT_F_V3);
     if (kflags == 0) kflags = LRT_F_SIMPLE;
     if (want_feat && !(kflags & LRT_F_SIMPLE))
@@ -1187,6 +1223,12 @@ int lrt_initialize(void) {
     LRT_HIP(hipMalloc(&g_ctx.d_queue, sizeof(unsigned int) * kQueueSlots));
     LRT_HIP(hipMalloc(&g_ctx.d_tiles, sizeof(unsigned long long) * kQueueSlots * kTileSetU64));
     LRT_HIP(hipMemset(g_ctx.d_tiles, 0, sizeof(unsigned long long) * kQueueSlots * kTileSetU64));
+    {   // parallel.cpp:262's lerpFac per frame number, divided once here instead of per wave
+        std::vector<float> t(kLerpTable);
+        for (int f = 0; f < kLerpTable; ++f) t[f] = (float)f / (float)(f + 1);
+        LRT_HIP(hipMalloc(&g_ctx.d_lerp, sizeof(float) * kLerpTable));
+        LRT_HIP(hipMemcpy(g_ctx.d_lerp, t.data(), sizeof(float) * kLerpTable, hipMemcpyHostToDevice));
+    }
     LRT_HIP(hipDeviceGetAttribute(&g_ctx.num_cus, hipDeviceAttributeMultiprocessorCount, dev));
     {   // keep freed stream-ordered blocks (the per-launch path-stack overflow) in the
         // pool instead of returning them to the driver at every synchronisation
@@ -1212,6 +1254,8 @@ int lrt_shutdown(void) {
     if (g_ctx.d_queue) (void)hipFree(g_ctx.d_queue);
     if (g_ctx.d_tiles) (void)hipFree(g_ctx.d_tiles);
     g_ctx.d_tiles = nullptr;
+    if (g_ctx.d_lerp) (void)hipFree(g_ctx.d_lerp);
+    g_ctx.d_lerp = nullptr;
     for (auto* f : g_ctx.d_feat)
         if (f) (void)hipFree(f);
     for (auto& m : g_ctx.masked_streams) (void)hipStreamDestroy(m.first);
@@ -1414,14 +1458,14 @@ int lrt_bvh_stats(const lrt_sphere* spheres, int count, const float* rays, int n
 }
 
 int lrt_libm_eval_host(int kind, const float* in, float* out, long long n) {
-    if (kind < 0 || kind > 3 || !in || !out || n < 0) return fail(LRT_E_INVALID, "invalid libm eval arguments");
+    if (kind < 0 || kind > 5 || !in || !out || n < 0) return fail(LRT_E_INVALID, "invalid libm eval arguments");
     for (long long i = 0; i < n; ++i)
         out[i] = libm_eval(kind, in[i]);
     return LRT_OK;
 }
 
 int lrt_libm_eval_device(int kind, const float* d_in, float* d_out, long long n) {
-    if (kind < 0 || kind > 3 || !d_in || !d_out || n < 0) return fail(LRT_E_INVALID, "invalid libm eval arguments");
+    if (kind < 0 || kind > 5 || !d_in || !d_out || n < 0) return fail(LRT_E_INVALID, "invalid libm eval arguments");
     if (n == 0) return LRT_OK;
     libm_kernel<<<(unsigned)((n + 255) / 256), 256, 0, nullptr>>>(kind, d_in, d_out, n);
     LRT_HIP(hipGetLastError());

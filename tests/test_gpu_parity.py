@@ -202,6 +202,31 @@ def test_libm_device_exhaustive_path_domain(gpu, manifest):
     del out
 
 
+def test_fast_sqrt_rcp_correctly_rounded(gpu):
+    """The device's short sqrt / reciprocal sequences (lrt_trace.h sqrt_rn, rcp_rn) equal
+    IEEE sqrtf and 1/x bit for bit: every mantissa at exponents around the fast paths'
+    limits and in the path's range, plus 2^24 random bit patterns (signs, zeros,
+    denormals, inf, NaN). tools/fpexact.hip checks all 2^32 inputs."""
+    import torch
+    from learnraytracing_amd import _lib as L
+    m = np.arange(1 << 23, dtype=np.uint32)
+    exps = [0, 1, 20, 23, 24, 30, 31, 32, 33, 100, 126, 127, 128, 150, 220, 250, 251, 252, 253, 254, 255]
+    pats = [m | np.uint32(e << 23) for e in exps]
+    pats.append(np.random.default_rng(5).integers(0, 1 << 32, 1 << 24, dtype=np.uint64).astype(np.uint32))
+    bits = np.concatenate(pats)
+    bits = np.concatenate([bits, bits | np.uint32(0x80000000)])
+    x = bits.view(np.float32)
+    with np.errstate(all="ignore"):
+        want = {4: np.sqrt(x), 5: np.float32(1.0) / x}
+    d_in = torch.from_numpy(x).cuda()
+    for kind, w in want.items():
+        d_out = torch.empty_like(d_in)
+        L.check(L.lib().lrt_libm_eval_device(kind, d_in.data_ptr(), d_out.data_ptr(), d_in.numel()))
+        got = d_out.cpu().numpy()
+        same = (got.view(np.uint32) == w.view(np.uint32)) | (np.isnan(got) & np.isnan(w))
+        assert same.all(), f"kind {kind}: {int((~same).sum())} mismatches, first x={x[~same][:4]}"
+
+
 def test_invalid_arguments_fail_loudly(gpu):
     from learnraytracing_amd import LrtError
     with pytest.raises(LrtError):
