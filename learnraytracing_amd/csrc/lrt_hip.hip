@@ -76,6 +76,7 @@ struct KernelArgs {
     int featMax;
     int regenMin;                 // v3: ended lanes that trigger a regeneration round
     const float* lerp;            // lerpFac = (float)f / (float)(f + 1) for f < kLerpTable (parallel.cpp:262)
+    float4* samp;                 // sample mode: frames planes of xc * rows colours
 };
 constexpr int kLerpTable = 1 << 16;
 
@@ -120,9 +121,15 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 // The grid is persistent (as many blocks as fit, grid-stride over tiles): short wave
 // tasks dispatched one per workgroup are limited by the workgroup dispatch rate
 // (~80 waves/us chip-wide measured), which left SIMDs at ~2 of 4 resident waves.
-template <int MAXD, bool kLds, bool kBvh, int kSplit, bool kFeat = false>
+//
+// kSamp (sample mode, several rounds per pixel and few pixels -- one GPU's row shard of a
+// multi-GPU frame): a wave task is ONE round of one tile, so tasks stay as short as at
+// one round per pixel; each lane stores its sample colour in a.samp (frame-major planes)
+// and merge_samples_kernel applies the lerp chain in frame order afterwards.
+template <int MAXD, bool kLds, bool kBvh, int kSplit, bool kFeat = false, bool kSamp = false>
 __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(const KernelArgs a) {
     static_assert(!kFeat || kSplit == 1, "feature launches keep a pixel's frames on one lane");
+    static_assert(!(kFeat && kSamp), "sample mode has no features");
     // LDS: [recursion stack kTraceLdsLevels x kBlock][powf tables][spheres][materials][lights][bvh stack]
     extern __shared__ float4 smem[];
     const int tid = threadIdx.x;
@@ -183,7 +190,8 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
     constexpr int kTileRows = kBlockWavesY * kWaveRows;
     constexpr int kTileX = kWaveCols * kBlockWavesX;
     const int tilesX = (a.xc + kTileX - 1) / kTileX;
-    const int ntiles = tilesX * ((a.rows + kTileRows - 1) / kTileRows);
+    const int rounds = kSamp ? (a.frames + kSplit - 1) / kSplit : 1;   // tasks per tile
+    const int ntiles = tilesX * ((a.rows + kTileRows - 1) / kTileRows) * rounds;
     const float invWidth = 1.0f / (float)a.width;     // parallel.cpp:260
     const float invHeight = 1.0f / (float)a.height;   // parallel.cpp:261
     const int fend = a.frame0 + a.frames;
@@ -198,14 +206,15 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
         // issued after this tile's loads (vmcnt retires in order, so a load issued behind
         // the atomic would wait for it) and consumed after the trace, which hides it.
         // (Prefetching the next tile's pixels as well costs VGPRs beyond the 128 cap.)
-        const int tile = q + kV0Queues * i;
+        const int task = q + kV0Queues * i;
+        const int tile = kSamp ? task / rounds : task;
         const int lx = (tile % tilesX) * kTileX + (wave % kBlockWavesX) * kWaveCols + (p % kWaveCols);
         const int ly = (tile / tilesX) * kTileRows + (wave / kBlockWavesX) * kWaveRows + (p / kWaveCols);
         const bool valid = lx < a.xc && ly < a.rows;
         const int x = a.x0 + lx;
         const int y = valid ? a.y0 + (ly / a.rb) * a.rb * a.rp + a.rph * a.rb + ly % a.rb : 0;
         float4* px = a.out + (size_t)ly * a.xc + lx;
-        float4 acc = valid ? *px : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        float4 acc = (valid && !kSamp) ? *px : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         float4 fb[6];   // feature running values (kFeat)
         const size_t pix = (size_t)ly * a.xc + lx;
         if constexpr (kFeat) {
@@ -215,7 +224,9 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
         }
         unsigned long long fetched = 0;
         if (LRT_V0_DYNAMIC && lane == 0) fetched = atomicAdd(ctr, 1ull);
-        for (int f0 = a.frame0; f0 < fend; f0 += kSplit) {
+        const int fbeg = kSamp ? a.frame0 + (task % rounds) * kSplit : a.frame0;
+        const int fstop = kSamp ? fbeg + kSplit : fend;
+        for (int f0 = fbeg; f0 < fstop; f0 += kSplit) {
             const int f = f0 + sub;
             F3 col = f3(0.0f, 0.0f, 0.0f);
             F3 feat[3] = {f3(0.0f, 0.0f, 0.0f), f3(0.0f, 0.0f, 0.0f), f3(0.0f, 0.0f, 0.0f)};
@@ -227,6 +238,11 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
                 Ray r = GetRay(a.cam, u, v, rng);
                 col = Trace<MAXD, kBvh, kFeat>(r, a.maxDepth, rays, rng, sc, smem + tid, kBlock, a.ovf + gtid,
                                                gthreads, a.ndl, feat);
+            }
+            if constexpr (kSamp) {   // the merge kernel lerps the planes in frame order
+                if (valid && f < fend)
+                    a.samp[(size_t)(f - a.frame0) * ((size_t)a.xc * a.rows) + pix] = make_float4(col.x, col.y, col.z, 0.0f);
+                continue;
             }
             // the group's colours go through this lane's (now free) stack level 0 in LDS:
             // one write, then one read per frame, instead of three shuffles per frame
@@ -266,7 +282,7 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
             }
             if (kSplit > 1) __builtin_amdgcn_wave_barrier();
         }
-        if (valid && sub == 0) *px = acc;
+        if (!kSamp && valid && sub == 0) *px = acc;
         if constexpr (kFeat) {
 #pragma unroll
             for (int k = 0; k < 6; ++k)
@@ -328,6 +344,26 @@ __global__ void rays_collect_kernel(unsigned long long* tiles, unsigned long lon
     }
     v = wave_sum(v);
     if (l == 0 && v) atomicAdd(rays, v);
+}
+
+// Sample mode's second half: TraceRowJob's progressive lerp (parallel.cpp:262,280-286)
+// over the frame planes in order, one thread per pixel (coalesced plane reads).
+__global__ void merge_samples_kernel(const float4* __restrict__ samp, float4* __restrict__ out, const float* lerp,
+                                     int npix, int frame0, int frames) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npix) return;
+    const float4 o = out[i];
+    F3 acc = f3(o.x, o.y, o.z);
+    for (int k = 0; k < frames; ++k) {
+        const float4 c = samp[(size_t)k * npix + i];
+        const int f = frame0 + k;
+        const float lerpFac = f < kLerpTable ? lerp[f] : (float)f / (float)(f + 1);
+        acc = acc * lerpFac + f3(c.x, c.y, c.z) * (1.0f - lerpFac);
+    }
+    float* d = reinterpret_cast<float*>(out + i);   // alpha untouched
+    d[0] = acc.x;
+    d[1] = acc.y;
+    d[2] = acc.z;
 }
 
 // Frame assembly: shard g's local row ly -> global row (as lrt_render_desc's map).
@@ -789,9 +825,28 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     int cus = g_ctx.num_cus;
     for (const auto& m : g_ctx.masked_streams)
         if (m.first == s) cus = m.second;
+    // Sample mode (kSamp): several rounds per pixel and fewer than 16 tasks per resident
+    // wave (a row shard of a multi-GPU frame at N x spp) -- one task per (tile, round)
+    // plus a merge pass, instead of one long task per tile (shard of 8: 7,200 tiles of 2
+    // rounds on 4,096 waves). LRT_SAMPLE_MODE=0 turns it off, 2 forces it (A/B, tests).
+    const int rounds = (a.frames + kSplit - 1) / kSplit;
+    const size_t npix = (size_t)xc * rows;
+    bool samp = false;
+    if constexpr (!kFeat && kSplit >= 4) {
+        static int mode = -1;
+        if (mode < 0) {
+            const char* v = getenv("LRT_SAMPLE_MODE");
+            mode = v ? atoi(v) : 1;
+        }
+        const long long slots = (long long)per_cu * cus;
+        samp = mode > 0 && lds && !a.bv.on && rounds >= 2 && npix * (size_t)a.frames * sizeof(float4) <= (2ull << 30) &&
+               (mode == 2 || ntiles < 16 * slots);
+    }
+    const long long tasks = samp ? ntiles * rounds : ntiles;
     long long blocks = (long long)per_cu * cus * LRT_V0_GRID_MULT;
-    if (blocks > ntiles) blocks = ntiles;
+    if (blocks > tasks) blocks = tasks;
     const dim3 grid((unsigned)blocks);
+    a.samp = nullptr;
     a.ovf = nullptr;
     a.tiles = g_ctx.d_tiles + (size_t)(g_ctx.tiles_next++ % kQueueSlots) * kTileSetU64;
 #ifdef LRT_EXP_SECSTATS
@@ -806,7 +861,23 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
         e = hipMallocAsync((void**)&a.ovf, sizeof(float4) * gthreads * (size_t)(a.maxDepth - kTraceLdsLevels), s);
         if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(trace stack overflow)");
     }
-    if (a.bv.on) {
+    if constexpr (!kFeat && kSplit >= 4) {
+        if (samp) {
+            e = hipMallocAsync((void**)&a.samp, sizeof(float4) * npix * (size_t)a.frames, s);
+            if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(sample planes)");
+            trace_kernel<MAXD, true, false, kSplit, false, true><<<grid, kBlock, ldsb, s>>>(a);
+            e = hipGetLastError();
+            if (e != hipSuccess) return hip_fail(e, "trace_kernel (samples) launch");
+            merge_samples_kernel<<<(unsigned)((npix + 255) / 256), 256, 0, s>>>(a.samp, a.out, a.lerp, (int)npix,
+                                                                               a.frame0, a.frames);
+            e = hipGetLastError();
+            if (e != hipSuccess) return hip_fail(e, "merge_samples_kernel launch");
+            e = hipFreeAsync(a.samp, s);
+            if (e != hipSuccess) return hip_fail(e, "hipFreeAsync(sample planes)");
+        }
+    }
+    if (samp) {
+    } else if (a.bv.on) {
         if (lds)
             trace_kernel<MAXD, true, true, kSplit, kFeat><<<grid, kBlock, ldsb, s>>>(a);
         else

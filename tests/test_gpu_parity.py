@@ -380,3 +380,30 @@ def test_v3_row_block_cyclic_shard(gpu):
     want, wrays = oracle.orc_render(w, h, 2, 8)
     _assert_bitwise(buf, want[rows][..., :3], "v3 shard")
     assert rays == sum(oracle.orc_render(w, h, 2, 8, y0=y, yc=1)[1] for y in rows)
+
+
+@pytest.mark.parametrize("case", [
+    (320, 90, 32, 8, 0),      # 2 rounds of 16 lanes per pixel, few tiles: sample mode
+    (200, 60, 40, 8, 3),      # 3 rounds, the last one partial, frame offset
+    (1280, 720, 32, 8, 0),    # rank 0's shard of 8 at N x spp, as bench --gpus 8 renders it
+])
+def test_many_frames_sample_mode_vs_oracle(gpu, case):
+    """More frames per pixel than lanes per pixel on few pixels runs in sample mode
+    (one task per tile and round, frame planes merged afterwards): same bits as the
+    oracle's serial per-pixel loop."""
+    w, h, frames, depth, f0 = case
+    if w == 1280:   # row-block-cyclic shard 0 of 8, blocks of 8 rows
+        rows = [y for y in range(h) if (y // 8) % 8 == 0]
+        job = gpu.Job(width=w, height=h, frame0=f0, frames=frames, max_depth=depth, row_block=8, row_period=8,
+                      row_phase=0)
+        buf = np.zeros((len(rows), w, 4), np.float32)
+        rays = gpu.render_host(job, buf)
+        yc = 24   # check the first three row blocks against the oracle (the rest is the same code)
+        want = np.concatenate([oracle.orc_render(w, h, frames, depth, frame0=f0, y0=y, yc=1)[0] for y in rows[:yc]])
+        _assert_bitwise(buf[:yc], want[..., :3], f"shard of 8 at {frames} spp")
+        assert rays > 0
+        return
+    buf, rays = _render(gpu, w, h, frames, depth, frame0=f0)
+    want, wrays = oracle.orc_render(w, h, frames, depth, frame0=f0)
+    _assert_bitwise(buf, want[..., :3], f"{case}")
+    assert rays == wrays
