@@ -283,30 +283,40 @@ LRT_DEV void SphereRoots(float rsProj, float ifHit, float tMin, float& closestT,
 // is the reference's; hit position and normal are computed once for the winner
 // (they are pure functions of (ray, t, sphere), so this is bit-identical to the
 // reference overwriting them on every closer hit).
-template <bool kBvh = false>
+// kNS > 0: the scene has exactly kNS spheres (the reference's kSphereCount is a compile-time
+// 9, parallel.cpp:27): the scan is fully unrolled with constant LDS offsets.
+template <bool kBvh = false, int kNS = 0>
 LRT_DEV int ClosestHitSV(const Ray& r, float tMin, float tMax, const SceneView& sc, float& tOut) {
     if (kBvh) return ClosestHitBVH(r.orig, r.dir, sc.bv, tOut, sc.bstk, sc.bstride);   // tMin/tMax = kMinT/kMaxT
     float closestT = tMax;
     int id = -1;
     const ConstFPtr csph = (ConstFPtr)sc.gsph;
     auto cload = [&](int i) { return make_float4(csph[4 * i], csph[4 * i + 1], csph[4 * i + 2], csph[4 * i + 3]); };
-    float4 next = LRT_SCALAR_SCENE ? cload(0) : sc.sph[0];   // one sphere ahead (SGPRs or VGPRs)
-    for (int i = 0; i < sc.count; ++i) {
-        const float4 s = next;
-        if (i + 1 < sc.count) next = LRT_SCALAR_SCENE ? cload(i + 1) : sc.sph[i + 1];
+    auto test = [&](int i, const float4& s) {
         F3 rs = f3(s.x, s.y, s.z) - r.orig;
         float rsProj = dot(rs, r.dir);
         float ifHit = dot(rs, rs) - rsProj * rsProj - s.w;
         SphereRoots(rsProj, ifHit, tMin, closestT, id, i);
+    };
+    if constexpr (kNS > 0) {
+#pragma unroll
+        for (int i = 0; i < kNS; ++i) test(i, sc.sph[i]);
+    } else {
+        float4 next = LRT_SCALAR_SCENE ? cload(0) : sc.sph[0];   // one sphere ahead (SGPRs or VGPRs)
+        for (int i = 0; i < sc.count; ++i) {
+            const float4 s = next;
+            if (i + 1 < sc.count) next = LRT_SCALAR_SCENE ? cload(i + 1) : sc.sph[i + 1];
+            test(i, s);
+        }
     }
     tOut = closestT;
     return id;
 }
-template <bool kBvh = false>
+template <bool kBvh = false, int kNS = 0>
 LRT_DEV bool HitWorld(const Ray& r, float tMin, float tMax, const SceneView& sc, Hit& outHit, int& outID) {
     float closestT;
     sec_count(sc, kSecHit);
-    const int id = ClosestHitSV<kBvh>(r, tMin, tMax, sc, closestT);
+    const int id = ClosestHitSV<kBvh, kNS>(r, tMin, tMax, sc, closestT);
     if (id < 0) return false;
     float4 s = sc.sph[id];
     outHit.pos = point_at(r, closestT);
@@ -334,7 +344,7 @@ struct DeferredLight {
     bool on;
 };
 
-template <bool kBvh = false>
+template <bool kBvh = false, int kNS = 0>
 LRT_DEV F3 ScatterDir(const Material& mat, int matId, const Ray& r_in, const Hit& rec, F3& outLightE,
                       int& inoutRayCount, uint32_t& rng, const SceneView& sc, DeferredLight* defer = nullptr) {
     outLightE = f3(0.0f, 0.0f, 0.0f);
@@ -386,7 +396,7 @@ LRT_DEV F3 ScatterDir(const Material& mat, int matId, const Ray& r_in, const Hit
                 const Ray sr = make_ray(rec.pos, l);
                 lit = ShadowReachesLightBVH(sr.orig, sr.dir, i, s, sc.bv, sc.bstk, sc.bstride);
             } else {
-                lit = ClosestHitSV<kBvh>(make_ray(rec.pos, l), kMinT, kMaxT, sc, tLight) == i;
+                lit = ClosestHitSV<kBvh, kNS>(make_ray(rec.pos, l), kMinT, kMaxT, sc, tLight) == i;
             }
             sec_enter(sc, kSecLambert, false);
             if (lit) {   // HitWorld && hitID == i
@@ -444,18 +454,18 @@ constexpr int kTraceLdsLevels = LRT_TRACE_LDS_LEVELS;
 #ifndef LRT_DUAL_HIT
 #define LRT_DUAL_HIT 1
 #endif
-template <int MAXD, bool kFeat, int kLdsLev>
+template <int MAXD, bool kFeat, int kLdsLev, int kNS>
 LRT_DEV F3 TraceDual(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const SceneView& sc,
                      float4* lstk, int lstride, float4* gstk, size_t gstride, int ndl, F3* feat);
 // ndl (LRT_F_NO_DOUBLE_LIGHT): the GL loop's doMaterialE rule (fragmentShader.fs.glsl:430,
 // 456-457) -- a scatter event reached through a Lambert bounce adds no emissive; the
 // terminating hit always does. kFeat: feat[0..2] receive the first hit's normal,
 // position and albedo (fragmentShader.fs.glsl:444-451; left untouched on a miss).
-template <int MAXD, bool kBvh = false, bool kFeat = false, int kLdsLev = kTraceLdsLevels>
+template <int MAXD, bool kBvh = false, bool kFeat = false, int kLdsLev = kTraceLdsLevels, int kNS = 0>
 LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const SceneView& sc,
                  float4* lstk, int lstride, float4* gstk, size_t gstride, int ndl = 0, F3* feat = nullptr) {
     if constexpr (!kBvh && LRT_DUAL_HIT)
-        return TraceDual<MAXD, kFeat, kLdsLev>(r, maxDepth, inoutRayCount, rng, sc, lstk, lstride, gstk, gstride,
+        return TraceDual<MAXD, kFeat, kLdsLev, kNS>(r, maxDepth, inoutRayCount, rng, sc, lstk, lstride, gstk, gstride,
                                                ndl, feat);
     auto put = [&](int lvl, float4 v) {
         if (MAXD <= kLdsLev || lvl < kLdsLev) lstk[lvl * lstride] = v;
@@ -472,7 +482,7 @@ LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const S
         Hit rec;
         int id = 0;
         ++inoutRayCount;
-        if (!HitWorld<kBvh>(r, kMinT, kMaxT, sc, rec, id)) {
+        if (!HitWorld<kBvh, kNS>(r, kMinT, kMaxT, sc, rec, id)) {
             float t = 0.5f * (r.dir.y + 1.0f);
             leaf = ((1.0f - t) * f3(1.0f, 1.0f, 1.0f) + t * f3(0.5f, 0.7f, 1.0f)) * 0.3f;
             break;
@@ -486,7 +496,7 @@ LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const S
         }
         if (depth < maxDepth) {   // :212
             F3 lightE;
-            const F3 X = ScatterDir<kBvh>(mat, id, r, rec, lightE, inoutRayCount, rng, sc);
+            const F3 X = ScatterDir<kBvh, kNS>(mat, id, r, rec, lightE, inoutRayCount, rng, sc);
             sec_count(sc, kSecPost);
             const F3 dir = normalize(normalize(X));
             if (mat.type != 1 || dot(dir, rec.normal) > 0.0f) {   // Metal absorbs (:147)
@@ -519,15 +529,13 @@ LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const S
 // values HitSphere computes for each ray (maths.cpp:54-59) -- and each ray keeps its own
 // shrinking closestT exactly as HitWorld does, so both results are bit-identical to two
 // separate scans. Saves the shadow ray's separate, partly occupied pass.
+template <int kNS = 0>
 LRT_DEV void DualClosestHit(const F3& o, const F3& db, bool hasShadow, const F3& ds, const SceneView& sc,
                             int& idB, float& tB, int& idS) {
     float closestB = kMaxT, closestS = kMaxT;
     idB = -1;
     idS = -1;
-    float4 next = sc.sph[0];
-    for (int i = 0; i < sc.count; ++i) {
-        const float4 s = next;
-        if (i + 1 < sc.count) next = sc.sph[i + 1];
+    auto test = [&](int i, const float4& s) {
         const F3 rs = f3(s.x, s.y, s.z) - o;
         const float rr = dot(rs, rs);
         {
@@ -540,6 +548,17 @@ LRT_DEV void DualClosestHit(const F3& o, const F3& db, bool hasShadow, const F3&
             const float ifHit = rr - rsProj * rsProj - s.w;
             SphereRoots(rsProj, ifHit, kMinT, closestS, idS, i);
         }
+    };
+    if constexpr (kNS > 0) {
+#pragma unroll
+        for (int i = 0; i < kNS; ++i) test(i, sc.sph[i]);
+    } else {
+        float4 next = sc.sph[0];
+        for (int i = 0; i < sc.count; ++i) {
+            const float4 s = next;
+            if (i + 1 < sc.count) next = sc.sph[i + 1];
+            test(i, s);
+        }
     }
     tB = closestB;
 }
@@ -547,7 +566,7 @@ LRT_DEV void DualClosestHit(const F3& o, const F3& db, bool hasShadow, const F3&
 // Trace for the linear scan with the closest hit of each bounce ray found at the end of
 // the previous iteration, in one pass with the last light's shadow ray (DualClosestHit).
 // Same events, draws, ray counts and accumulation order as Trace.
-template <int MAXD, bool kFeat = false, int kLdsLev = kTraceLdsLevels>
+template <int MAXD, bool kFeat = false, int kLdsLev = kTraceLdsLevels, int kNS = 0>
 LRT_DEV F3 TraceDual(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const SceneView& sc,
                      float4* lstk, int lstride, float4* gstk, size_t gstride, int ndl, F3* feat) {
     auto put = [&](int lvl, float4 v) {
@@ -564,7 +583,7 @@ LRT_DEV F3 TraceDual(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, con
     Hit rec;
     int id = 0;
     ++inoutRayCount;
-    bool hit = HitWorld<false>(r, kMinT, kMaxT, sc, rec, id);
+    bool hit = HitWorld<false, kNS>(r, kMinT, kMaxT, sc, rec, id);
     for (;;) {
         if (!hit) {
             float t = 0.5f * (r.dir.y + 1.0f);
@@ -582,7 +601,7 @@ LRT_DEV F3 TraceDual(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, con
             F3 lightE;
             DeferredLight dl;
             dl.on = false;
-            const F3 X = ScatterDir<false>(mat, id, r, rec, lightE, inoutRayCount, rng, sc, &dl);
+            const F3 X = ScatterDir<false, kNS>(mat, id, r, rec, lightE, inoutRayCount, rng, sc, &dl);
             sec_count(sc, kSecPost);
             const F3 dir = normalize(normalize(X));
             if (mat.type != 1 || dot(dir, rec.normal) > 0.0f) {   // Metal absorbs (:147)
@@ -591,7 +610,7 @@ LRT_DEV F3 TraceDual(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, con
                 sec_count(sc, kSecHit);
                 int nid, sid;
                 float nt;
-                DualClosestHit(rec.pos, dir, dl.on, dl.l, sc, nid, nt, sid);
+                DualClosestHit<kNS>(rec.pos, dir, dl.on, dl.l, sc, nid, nt, sid);
                 if (dl.on && sid == dl.li) lightE = lightE + dl.contrib;
                 sec_enter(sc, kSecPost, false);
                 if (ndl && prevLambert) matE = f3(0.0f, 0.0f, 0.0f);
