@@ -348,7 +348,7 @@ __global__ __launch_bounds__(64, LRT_V3_WAVES_PER_EU) void regen_kernel(const Ke
 #endif
     // one ray-count atomic per block (same-address atomics serialise in one L2 channel)
     const unsigned long long total = wave_sum((unsigned long long)rays);
-    if (lane == 0 && total) atomicAdd(a.tiles + (kV0Queues + q) * kCtrStride, total);
+    if (lane == 0) block_epilogue(a.tiles, a.rays, q, bq, total);
 }
 
 }  // namespace lrt
