@@ -172,7 +172,12 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
         }
         for (int i = tid; i < 32; i += kBlock) reinterpret_cast<uint64_t*>(s_pow + 32)[i] = g.exp2[i];
     }
-    float4* s_sph = smem + kTraceLdsLevels * kBlock + kPowTableBytes / 16;
+    // renormalize() table after the powf tables (not in BVH launches: their 16 waves/CU
+    // have no LDS to spare)
+    constexpr int kLutBytes = kBvh ? 0 : kRenormBytes;
+    float* s_lut = kBvh ? nullptr : reinterpret_cast<float*>(s_pow + 64);
+    if (!kBvh) renorm_lut_fill(s_lut, tid, kBlock);
+    float4* s_sph = smem + kTraceLdsLevels * kBlock + (kPowTableBytes + kLutBytes) / 16;
     float4* s_mat = s_sph + a.count;
     int* s_lights = reinterpret_cast<int*>(s_mat + 3 * a.count);
     if (kLds) {
@@ -185,6 +190,7 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
     sc.pow.invc = s_pow;
     sc.pow.logc = s_pow + 16;
     sc.pow.exp2 = reinterpret_cast<const uint64_t*>(s_pow + 32);
+    sc.rnlut = s_lut;
     sc.sph = kLds ? s_sph : a.sph;
     sc.gsph = a.sph;
     sc.mats = kLds ? s_mat : a.mats;
@@ -263,7 +269,7 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
                 sec_count(sc, kSecCamera);
                 float u = ((float)x + RandomFloat01(rng)) * invWidth;              // :272
                 float v = ((float)y + RandomFloat01(rng)) * invHeight;             // :273
-                Ray r = GetRay(a.cam, u, v, rng);
+                Ray r = GetRay(a.cam, u, v, rng, sc.rnlut);
                 col = Trace<MAXD, kBvh, kFeat, kTraceLdsLevels, kNS>(r, a.maxDepth, rays, rng, sc, smem + tid, kBlock, a.ovf + gtid,
                                                gthreads, a.ndl, feat);
             }
@@ -820,7 +826,7 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     constexpr int kTileRows = kBlockWavesY * (64 / kSplit / WaveCols(kSplit));
     constexpr int kTileX = WaveCols(kSplit) * kBlockWavesX;
     const long long ntiles = (long long)((xc + kTileX - 1) / kTileX) * ((rows + kTileRows - 1) / kTileRows);
-    const size_t stack = sizeof(float4) * kTraceLdsLevels * kBlock + kPowTableBytes;
+    const size_t stack = sizeof(float4) * kTraceLdsLevels * kBlock + kPowTableBytes + (a.bv.on ? 0 : kRenormBytes);
     const size_t scene = lds ? sizeof(float4) * (4 * (size_t)a.count + (size_t)(a.nlights + 3) / 4 + 1) : 0;
     a.bvh_stack_offset = (int)(stack + scene);
     // v0 sizes the LDS traversal stack to this scene's BVH depth (1000 spheres: ~9
@@ -955,7 +961,7 @@ template <int MAXD, int kSplit>
 int launch_regen(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     constexpr int kTileRows = 8 / kSplit;
     const long long ntiles = (long long)((xc + 7) / 8) * ((rows + kTileRows - 1) / kTileRows);
-    const size_t stack = sizeof(float4) * kTraceLdsLevels * 64 + kPowTableBytes;
+    const size_t stack = sizeof(float4) * kTraceLdsLevels * 64 + kPowTableBytes + kRenormBytes;
     const size_t scene = lds ? sizeof(float4) * (4 * (size_t)a.count + (size_t)(a.nlights + 3) / 4 + 1) : 0;
     a.bvh_stack_offset = (int)(stack + scene);
     const size_t bstk = a.bv.on ? sizeof(unsigned short) * g_ctx.bvh_stack_levels * 64 : 0;

@@ -46,7 +46,9 @@ __device__ __forceinline__ SceneView stage_scene(const KernelArgs& a, float4* sm
         }
         for (int i = tid; i < 32; i += block) reinterpret_cast<uint64_t*>(s_pow + 32)[i] = g.exp2[i];
     }
-    float4* s_sph = smem + kTraceLdsLevels * block + kPowTableBytes / 16;
+    float* s_lut = reinterpret_cast<float*>(s_pow + 64);   // renormalize() table
+    renorm_lut_fill(s_lut, tid, block);
+    float4* s_sph = smem + kTraceLdsLevels * block + (kPowTableBytes + kRenormBytes) / 16;
     float4* s_mat = s_sph + a.count;
     int* s_lights = reinterpret_cast<int*>(s_mat + 3 * a.count);
     if (kLds) {
@@ -59,6 +61,7 @@ __device__ __forceinline__ SceneView stage_scene(const KernelArgs& a, float4* sm
     sc.pow.invc = s_pow;
     sc.pow.logc = s_pow + 16;
     sc.pow.exp2 = reinterpret_cast<const uint64_t*>(s_pow + 32);
+    sc.rnlut = s_lut;
     sc.sph = kLds ? s_sph : a.sph;
     sc.gsph = a.sph;
     sc.mats = kLds ? s_mat : a.mats;
@@ -250,7 +253,7 @@ __global__ __launch_bounds__(64, LRT_V3_WAVES_PER_EU) void regen_kernel(const Ke
                     rng = PixelSeed((uint32_t)px, (uint32_t)py, (uint32_t)f);
                     const float u = ((float)px + RandomFloat01(rng)) * invWidth;          // :272
                     const float v = ((float)py + RandomFloat01(rng)) * invHeight;         // :273
-                    r = GetRay(a.cam, u, v, rng);
+                    r = GetRay(a.cam, u, v, rng, sc.rnlut);
                     depth = 0;
                     prevLambert = false;
                     pend = false;
@@ -315,7 +318,7 @@ __global__ __launch_bounds__(64, LRT_V3_WAVES_PER_EU) void regen_kernel(const Ke
                 dl.on = false;
                 const F3 X = ScatterDir<kBvh>(mat, id, r, rec, lightE, rays, rng, sc, kBvh ? nullptr : &dl);
                 sec_count(sc, kSecPost);
-                const F3 dir = normalize(normalize(X));
+                const F3 dir = renormalize(normalize(X), sc.rnlut);
                 if (mat.type != 1 || dot(dir, nrm) > 0.0f) {   // Metal absorbs (:147)
                     if (a.ndl && prevLambert) matE = f3(0.0f, 0.0f, 0.0f);
                     prevLambert = mat.type == 0;

@@ -86,6 +86,19 @@ LRT_DEV float rcp_rn(float x) {
 }
 LRT_DEV float length(F3 v) { return sqrt_rn(v.x * v.x + v.y * v.y + v.z * v.z); } // maths.h:15
 LRT_DEV F3 normalize(F3 v) { float k = rcp_rn(length(v)); return f3(v.x * k, v.y * k, v.z * k); } // maths.h:93
+// normalize() of a vector that is already unit length to a few ulps (the reference
+// normalises twice: every Ray ctor normalises its direction again, maths.h:133-137).
+// Its |y|^2 lies within kRenormR ulps of 1, so 1/sqrt(|y|^2) comes from a table of
+// rcp_rn(sqrt_rn(d)) for those d, filled with the very same operations (renorm_lut_fill):
+// same bits as normalize(y) with ~12 fewer instructions. Any other |y|^2 computes.
+constexpr int kRenormR = 64;
+constexpr int kRenormBytes = ((2 * kRenormR + 1) * 4 + 15) / 16 * 16;
+LRT_DEV void renorm_lut_fill(float* lut, int tid, int block) {
+    for (int j = tid; j <= 2 * kRenormR; j += block) {
+        const float d = __int_as_float(0x3f800000 + j - kRenormR);
+        lut[j] = rcp_rn(sqrt_rn(d));
+    }
+}
 LRT_DEV F3 normalize_member(F3 v) { float l = length(v); return f3(v.x / l, v.y / l, v.z / l); } // maths.h:19
 LRT_DEV F3 reflect(F3 v, F3 n) { return v + 2.0f * (-dot(v, n) * n); }             // maths.h:100-103
 LRT_DEV bool refract(F3 v, F3 n, float nint, F3& out) {                             // maths.h:106-118
@@ -108,6 +121,15 @@ struct Ray {                                                                    
     F3 orig, dir;
 };
 LRT_DEV Ray make_ray(F3 o, F3 d) { Ray r; r.orig = o; r.dir = normalize(d); return r; }
+LRT_DEV F3 renormalize(F3 y, const float* lut) {
+    if (!lut) return normalize(y);
+    const float d = y.x * y.x + y.y * y.y + y.z * y.z;   // length()'s sum, same order
+    const int j = __float_as_int(d) - 0x3f800000 + kRenormR;
+    float k;
+    if ((unsigned)j <= 2u * kRenormR) k = lut[j];
+    else k = rcp_rn(sqrt_rn(d));
+    return f3(y.x * k, y.y * k, y.z * k);
+}
 LRT_DEV F3 point_at(const Ray& r, float t) { return r.orig + r.dir * t; }
 
 struct Hit { F3 pos, normal; float t; };                                            // maths.h:148-153
@@ -207,6 +229,7 @@ struct SceneView {
     unsigned short* bstk;              // this lane's BVH traversal stack (LDS)
     int bstride;
     libm::PowTables pow;               // powf tables for Dielectric's schlick (LDS copy)
+    const float* rnlut;                // renormalize() table (LDS), null: plain normalize
 #ifdef LRT_EXP_SECSTATS
     unsigned long long* secstats;      // diagnostic: per section {wave executions, active lanes, cycles}
     unsigned long long* sectime;       // this wave's LDS bookkeeping
@@ -384,7 +407,7 @@ LRT_DEV F3 ScatterDir(const Material& mat, int matId, const Ray& r_in, const Hit
                 float d = dot(l, nl);
                 float mx = (0.0f < d) ? d : 0.0f;   // std::max(0.0f, d)
                 const float4 e = sc.mats[3 * i + 1];
-                defer->l = normalize(l);   // the shadow Ray's ctor normalises again (maths.h:133-137)
+                defer->l = renormalize(l, sc.rnlut);   // the shadow Ray's ctor normalises again (maths.h:133-137)
                 defer->contrib = (mat.albedo * f3(e.x, e.y, e.z)) * (mx * omega / kPI);
                 defer->li = i;
                 defer->on = true;
@@ -393,10 +416,15 @@ LRT_DEV F3 ScatterDir(const Material& mat, int matId, const Ray& r_in, const Hit
             sec_count(sc, kSecShadow);
             bool lit;
             if constexpr (kBvh) {
-                const Ray sr = make_ray(rec.pos, l);
+                Ray sr;
+                sr.orig = rec.pos;
+                sr.dir = renormalize(l, sc.rnlut);
                 lit = ShadowReachesLightBVH(sr.orig, sr.dir, i, s, sc.bv, sc.bstk, sc.bstride);
             } else {
-                lit = ClosestHitSV<kBvh, kNS>(make_ray(rec.pos, l), kMinT, kMaxT, sc, tLight) == i;
+                Ray sr;
+                sr.orig = rec.pos;
+                sr.dir = renormalize(l, sc.rnlut);
+                lit = ClosestHitSV<kBvh, kNS>(sr, kMinT, kMaxT, sc, tLight) == i;
             }
             sec_enter(sc, kSecLambert, false);
             if (lit) {   // HitWorld && hitID == i
@@ -498,7 +526,7 @@ LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const S
             F3 lightE;
             const F3 X = ScatterDir<kBvh, kNS>(mat, id, r, rec, lightE, inoutRayCount, rng, sc);
             sec_count(sc, kSecPost);
-            const F3 dir = normalize(normalize(X));
+            const F3 dir = renormalize(normalize(X), sc.rnlut);
             if (mat.type != 1 || dot(dir, rec.normal) > 0.0f) {   // Metal absorbs (:147)
                 if (ndl && prevLambert) matE = f3(0.0f, 0.0f, 0.0f);
                 prevLambert = mat.type == 0;
@@ -603,7 +631,7 @@ LRT_DEV F3 TraceDual(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, con
             dl.on = false;
             const F3 X = ScatterDir<false, kNS>(mat, id, r, rec, lightE, inoutRayCount, rng, sc, &dl);
             sec_count(sc, kSecPost);
-            const F3 dir = normalize(normalize(X));
+            const F3 dir = renormalize(normalize(X), sc.rnlut);
             if (mat.type != 1 || dot(dir, rec.normal) > 0.0f) {   // Metal absorbs (:147)
                 // the next Trace's HitWorld (:204) and the deferred shadow ray (:122-123)
                 ++inoutRayCount;
@@ -649,10 +677,13 @@ struct CameraDev {   // maths.h:217-224
     F3 origin, a, u, r, llc, horiz, vert;
     float lensRadius;
 };
-LRT_DEV Ray GetRay(const CameraDev& c, float s, float t, uint32_t& rng) {   // maths.h:205-215
+LRT_DEV Ray GetRay(const CameraDev& c, float s, float t, uint32_t& rng, const float* lut = nullptr) {   // maths.h:205-215
     F3 rd = c.lensRadius * RandomInUnitDisk(rng);
     F3 offset = c.r * rd.x + c.u * rd.y;
-    return make_ray(c.origin + offset, normalize(c.llc + s * c.horiz + t * c.vert - c.origin - offset));
+    Ray r;
+    r.orig = c.origin + offset;
+    r.dir = renormalize(normalize(c.llc + s * c.horiz + t * c.vert - c.origin - offset), lut);
+    return r;
 }
 
 LRT_DEV uint32_t PixelSeed(uint32_t x, uint32_t y, uint32_t f) { return (x * 1973u + y * 9277u + f * 26699u) | 1u; }
