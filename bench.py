@@ -95,7 +95,7 @@ def cpu_baseline(cfg, budget_s: float):
 def kernel_name(kernel: str, frames: int) -> str:
     if kernel == "auto":   # mirrors render_device's policy in lrt_hip.hip
         kernel = "v0"
-    return {"v0": "trace_kernel", "v1": "paths_kernel", "v3": "regen_kernel"}.get(kernel, "paths2_kernel")
+    return {"v0": "trace_kernel", "v1": "paths_kernel", "v3": "regen_kernel", "wf": "wf_extend"}.get(kernel, "paths2_kernel")
 
 
 def read_traffic(cfg_name: str):
@@ -146,7 +146,7 @@ def main():
     ap.add_argument("--scene-global", action="store_true", help="read spheres from global memory, not LDS")
     ap.add_argument("--reserve-cus", type=int, default=None,
                     help="CUs the render stream leaves free for other streams (default 0)")
-    ap.add_argument("--kernel", choices=["auto", "v0", "v1", "v2", "v2s", "v3"], default="auto",
+    ap.add_argument("--kernel", choices=["auto", "v0", "v1", "v2", "v2s", "v3", "wf"], default="auto",
                     help="auto: the library's policy (default); v0: one pixel per lane (LRT_F_SIMPLE); "
                          "v1: unscheduled state machine; v2: phase-scheduled persistent; v2s[N]: "
                          "phase-scheduled, N static pixels per lane")
@@ -206,7 +206,7 @@ def main():
     rb = H if shards == 1 else args.row_block
     max_rows = max_shard_rows(H, rb, shards)
     rows = shard_rows(H, rb, shards, rank)
-    flags = (1 if args.scene_global else 0) | {"auto": 0, "v0": 2, "v1": 4, "v2": 16, "v2s": 8, "v3": 128}[args.kernel]
+    flags = (1 if args.scene_global else 0) | {"auto": 0, "v0": 2, "v1": 4, "v2": 16, "v2s": 8, "v3": 128, "wf": 256}[args.kernel]
     job = lrt.Job(width=W, height=H, frame0=0, frames=spp_total, max_depth=D, row_block=rb,
                   row_period=shards, row_phase=rank, row_count=rows, flags=flags)
     dev = torch.device("cuda", torch.cuda.current_device())

@@ -117,6 +117,10 @@ typedef struct lrt_render_desc {
                                 wave (a lane traces its pixel's frames in turn; ended
                                 lanes are refilled together from the wave's pixel
                                 stream). No lrt_features.                              */
+#define LRT_F_WAVEFRONT 256  /* v4: wavefront (breadth-first) path tracing: path state in
+                                HBM, closest-hit and per-material shading kernels over
+                                compacted queues, frame planes merged in order. No
+                                lrt_features.                                          */
 
 /* ---- the reference API (parallel.h:6-8) ---------------------------------- */
 

@@ -365,6 +365,7 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
 }  // namespace lrt
 #include "lrt_regen.h"
 namespace lrt {
+// (lrt_wavefront.h follows merge_samples_kernel)
 
 
 // Sample mode's second half: TraceRowJob's progressive lerp (parallel.cpp:262,280-286)
@@ -386,6 +387,10 @@ __global__ void merge_samples_kernel(const float4* __restrict__ samp, float4* __
     d[1] = acc.y;
     d[2] = acc.z;
 }
+
+}  // namespace lrt
+#include "lrt_wavefront.h"
+namespace lrt {
 
 // Frame assembly: shard g's local row ly -> global row (as lrt_render_desc's map).
 __global__ void unshard_kernel(const float4* __restrict__ src, float4* __restrict__ dst, int width, int height,
@@ -446,6 +451,11 @@ struct Context {
     unsigned queue_next = 0;
     unsigned long long* d_tiles = nullptr;   // kQueueSlots x v0 counter sets (trace_kernel)
     float* d_lerp = nullptr;                 // kLerpTable lerp factors (host IEEE division)
+    struct Wavefront {                       // v4 path state, grown on demand
+        void* buf = nullptr;
+        size_t bytes = 0;
+        unsigned long long* rayp = nullptr;  // 16 ray-count partials
+    } wf;
     unsigned tiles_next = 0;
     hipStream_t stream = nullptr;
     int count = 0, nlights = 0;
@@ -1025,6 +1035,102 @@ int launch_regen_split(const KernelArgs& a, bool lds, int xc, int rows, int fram
     return launch_regen<MAXD, 1>(a, lds, xc, rows, s);
 }
 
+// v4 (lrt_wavefront.h): chunks of whole pixels, maxDepth + 1 extend/shade rounds each,
+// then the chunk's frame planes merged into the window. Path state is ~100 B + 16 B per
+// recursion level per pixel-sample; chunks are sized to a 2 GB budget.
+int launch_wavefront(KernelArgs a, bool lds, hipStream_t s) {
+    const int frames = a.frames, levels = std::max(1, a.maxDepth);
+    const size_t npix = (size_t)a.xc * a.rows;
+    const size_t per_path = 4 + 4 * 16 + 16 + 5 * 4 + 16 * (size_t)levels;
+    const size_t budget = (size_t)2 << 30;
+    size_t cpix = std::max<size_t>(1, budget / (per_path * (size_t)frames));
+    cpix = std::min(cpix, npix);
+    const size_t C = cpix * (size_t)frames;
+    if (C > 0x7fffffff) return fail(LRT_E_INVALID, "wavefront chunk too large");
+    // the persistent grid: every wavefront kernel runs B blocks, block j on region j
+    const size_t head = kPowTableBytes + kRenormBytes;
+    const size_t scene = lds ? sizeof(float4) * (4 * (size_t)a.count + (size_t)(a.nlights + 3) / 4 + 1) : 0;
+    const size_t bstk = a.bv.on ? sizeof(unsigned short) * g_ctx.bvh_stack_levels * kWfBlock : 0;
+    const size_t ldsb = head + scene + bstk;
+    const bool bvh = a.bv.on != 0, fixed = lds && !bvh && a.count == kFixedSpheres;
+    const void* kx = bvh ? (const void*)wf_extend<true, 0> : fixed ? (const void*)wf_extend<false, kFixedSpheres>
+                                                                   : (const void*)wf_extend<false, 0>;
+    const void* ks = bvh ? (const void*)wf_shade<true, 0> : fixed ? (const void*)wf_shade<false, kFixedSpheres>
+                                                                  : (const void*)wf_shade<false, 0>;
+    int per_cu = 0, per_cu_s = 0;
+    hipError_t e = occupancy(&per_cu, kx, kWfBlock, ldsb);
+    if (e == hipSuccess) e = occupancy(&per_cu_s, ks, kWfBlock, ldsb);
+    if (e != hipSuccess) return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
+    per_cu = std::min(per_cu, per_cu_s);
+    if (per_cu < 1) return fail(LRT_E_INVALID, "wavefront kernels do not fit on a CU");
+    const int B = per_cu * g_ctx.num_cus;
+    const size_t cnt_bytes = sizeof(unsigned int) * 4 * (size_t)(a.maxDepth + 2) * B;
+    const size_t need = per_path * (C + (size_t)B) + cnt_bytes + 256 * 12;
+    auto& wf = g_ctx.wf;
+    if (wf.bytes < need) {
+        if (wf.buf) (void)hipFree(wf.buf);
+        wf.buf = nullptr;
+        wf.bytes = 0;
+        if (hipMalloc(&wf.buf, need) != hipSuccess) return fail(LRT_E_NOMEM, "hipMalloc(wavefront state)");
+        wf.bytes = need;
+    }
+    if (!wf.rayp) {
+        LRT_HIP(hipMalloc(&wf.rayp, sizeof(unsigned long long) * kV0Queues * kCtrStride));
+        LRT_HIP(hipMemset(wf.rayp, 0, sizeof(unsigned long long) * kV0Queues * kCtrStride));
+    }
+    WfArgs w;
+    w.a = a;
+    char* b = static_cast<char*>(wf.buf);
+    auto take = [&](size_t bytes) { void* p = b; b += (bytes + 255) / 256 * 256; return p; };
+    const size_t qslots = C + (size_t)B;   // B regions of R0 = ceil(C / B) state slots
+    w.o = static_cast<float4*>(take(16 * qslots));
+    w.d = static_cast<float4*>(take(16 * qslots));
+    w.sl = static_cast<float4*>(take(16 * qslots));
+    w.lit = static_cast<float4*>(take(16 * qslots));
+    w.samp = static_cast<float4*>(take(16 * C));
+    w.stack = static_cast<float4*>(take(16 * qslots * (size_t)levels));
+    w.rng = static_cast<uint32_t*>(take(4 * qslots));
+    w.qa[0] = static_cast<uint32_t*>(take(4 * qslots));
+    w.qa[1] = static_cast<uint32_t*>(take(4 * qslots));
+    for (int t = 0; t < 3; ++t) w.qm[t] = static_cast<uint32_t*>(take(4 * qslots));
+    w.cnt = static_cast<unsigned int*>(take(cnt_bytes));
+    w.rayp = wf.rayp;
+    // LDS: [powf tables][renormalize table][scene if staged][bvh traversal stack]
+    w.lds = lds ? 1 : 0;
+    w.bstk_off = (int)(head + scene);
+    const dim3 grid((unsigned)B), block(kWfBlock);
+    for (size_t pix0 = 0; pix0 < npix; pix0 += cpix) {
+        const size_t cp = std::min(cpix, npix - pix0);
+        w.pix0 = (int)pix0;
+        w.cpix = (int)cp;
+        w.C = (int)(cp * (size_t)frames);
+        w.R0 = (int)((w.C + B - 1) / B);
+        w.Cs = w.R0 * B;
+        LRT_HIP(hipMemsetAsync(w.cnt, 0, cnt_bytes, s));
+        wf_camera<<<grid, block, kRenormBytes, s>>>(w);
+        for (int it = 0; it <= a.maxDepth; ++it) {
+            if (bvh) {
+                wf_extend<true, 0><<<grid, block, ldsb, s>>>(w, it);
+                wf_shade<true, 0><<<grid, block, ldsb, s>>>(w, it);
+            } else if (fixed) {
+                wf_extend<false, kFixedSpheres><<<grid, block, ldsb, s>>>(w, it);
+                wf_shade<false, kFixedSpheres><<<grid, block, ldsb, s>>>(w, it);
+            } else {
+                wf_extend<false, 0><<<grid, block, ldsb, s>>>(w, it);
+                wf_shade<false, 0><<<grid, block, ldsb, s>>>(w, it);
+            }
+        }
+        merge_samples_kernel<<<(unsigned)((cp + 255) / 256), 256, 0, s>>>(w.samp, a.out + pix0, a.lerp, (int)cp,
+                                                                         a.frame0, a.frames);
+        e = hipGetLastError();
+        if (e != hipSuccess) return hip_fail(e, "wavefront launch");
+    }
+    wf_rays_collect<<<1, 64, 0, s>>>(wf.rayp, a.rays);
+    e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "wavefront ray collect");
+    return LRT_OK;
+}
+
 template <bool kLdsScene, bool kV2, bool kOverflow, int kPix = 0, bool kBvh = false>
 int launch_paths(PathArgs& a, hipStream_t s) {
     constexpr bool kStaticPixel = kPix > 0;
@@ -1152,12 +1258,13 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     // for v2s); v1/v2/v2s stay selectable for A/B.
     a.regenMin = 0;
     a.lerp = g_ctx.d_lerp;
-    int kflags = d->flags & (LRT_F_SIMPLE | LRT_F_V1 | LRT_F_V2S | LRT_F_V2 | LRT_F_V3);
+    int kflags = d->flags & (LRT_F_SIMPLE | LRT_F_V1 | LRT_F_V2S | LRT_F_V2 | LRT_F_V3 | LRT_F_WAVEFRONT);
     if (kflags == 0) kflags = LRT_F_SIMPLE;
     if (want_feat && !(kflags & LRT_F_SIMPLE))
         return fail(LRT_E_INVALID, "features are implemented by the v0 kernel only");
-    if (a.ndl && !(kflags & (LRT_F_SIMPLE | LRT_F_V3)))
-        return fail(LRT_E_INVALID, "LRT_F_NO_DOUBLE_LIGHT is implemented by the v0 and v3 kernels only");
+    if (a.ndl && !(kflags & (LRT_F_SIMPLE | LRT_F_V3 | LRT_F_WAVEFRONT)))
+        return fail(LRT_E_INVALID, "LRT_F_NO_DOUBLE_LIGHT is implemented by the v0, v3 and wavefront kernels only");
+    if (kflags & LRT_F_WAVEFRONT) return launch_wavefront(a, lds, s);
     if (kflags & LRT_F_V3) {
         if (d->max_depth <= 8) return launch_regen_split<8>(a, lds, d->x_count, d->row_count, d->frames, s);
         if (d->max_depth <= 20) return launch_regen_split<20>(a, lds, d->x_count, d->row_count, d->frames, s);
@@ -1352,6 +1459,9 @@ int lrt_shutdown(void) {
     g_ctx.d_tiles = nullptr;
     if (g_ctx.d_lerp) (void)hipFree(g_ctx.d_lerp);
     g_ctx.d_lerp = nullptr;
+    if (g_ctx.wf.buf) (void)hipFree(g_ctx.wf.buf);
+    if (g_ctx.wf.rayp) (void)hipFree(g_ctx.wf.rayp);
+    g_ctx.wf = Context::Wavefront();
     for (auto* f : g_ctx.d_feat)
         if (f) (void)hipFree(f);
     for (auto& m : g_ctx.masked_streams) (void)hipStreamDestroy(m.first);

@@ -244,7 +244,7 @@ def test_deterministic_repeat_full_config2(gpu):
 
 
 @pytest.mark.parametrize("n,seed", [(17, 3), (200, 5), (1000, 1), (4096, 7)])
-@pytest.mark.parametrize("kflags", [2, 8, 16, 128])
+@pytest.mark.parametrize("kflags", [2, 8, 16, 128, 256])
 def test_bvh_equals_linear_scan(gpu, n, seed, kflags):
     """The BVH closest hit returns the reference's scan result bit for bit: same
     pixels and ray counts as LRT_F_NO_BVH, for every kernel."""
@@ -318,11 +318,14 @@ def test_cu_reserved_render_stream(gpu):
 
 
 V3 = 128   # LRT_F_V3: path regeneration inside the wave
+WF = 256   # LRT_F_WAVEFRONT: breadth-first kernels over compacted queues
+ALT = pytest.mark.parametrize("kflags", [V3, WF], ids=["v3", "wavefront"])
 
 
-def test_v3_config2_full_frame_vs_oracle(gpu):
-    """v3 on BASELINE config 2 at full size, bit-exact vs the C oracle."""
-    buf, rays = _render(gpu, 1280, 720, 4, 8, flags=V3)
+@ALT
+def test_v3_config2_full_frame_vs_oracle(gpu, kflags):
+    """v3 and the wavefront kernels on BASELINE config 2 at full size, bit-exact vs the C oracle."""
+    buf, rays = _render(gpu, 1280, 720, 4, 8, flags=kflags)
     want, wrays = oracle.orc_render(1280, 720, 4, 8)
     _assert_bitwise(buf, want[..., :3], "v3 config2 full frame")
     assert rays == wrays
@@ -334,15 +337,17 @@ def test_v3_config2_full_frame_vs_oracle(gpu):
     (1920, 1080, 16, 50, 0, 0, None, 520, 24), # config 3 band: deep paths, overflow stack
     (33, 9, 1, 8, 0, 0, None, 0, None),        # fewer pixels than one wave per queue
 ])
-def test_v3_windows_vs_oracle(gpu, case):
+@ALT
+def test_v3_windows_vs_oracle(gpu, case, kflags):
     w, h, frames, depth, f0, x0, xc, y0, yc = case
-    buf, rays = _render(gpu, w, h, frames, depth, frame0=f0, x0=x0, xc=xc, y0=y0, yc=yc, flags=V3)
+    buf, rays = _render(gpu, w, h, frames, depth, frame0=f0, x0=x0, xc=xc, y0=y0, yc=yc, flags=kflags)
     want, wrays = oracle.orc_render(w, h, frames, depth, frame0=f0, x0=x0, xc=xc, y0=y0, yc=yc)
     _assert_bitwise(buf, want[..., :3], f"v3 {case}")
     assert rays == wrays
 
 
-def test_v3_fuzz_and_scene1000(gpu, manifest, images):
+@ALT
+def test_v3_fuzz_and_scene1000(gpu, manifest, images, kflags):
     """v3 on the fuzzed scenes (all materials, TIR, 1-3 lights) and the 1000-sphere crops."""
     from learnraytracing_amd import _lib as L
     from learnraytracing_amd.scene import scene_from_arrays
@@ -355,26 +360,27 @@ def test_v3_fuzz_and_scene1000(gpu, manifest, images):
             for i, n in enumerate(names):
                 setattr(cam, n, L.f3(*vals[3 * i:3 * i + 3]))
             cam.lensRadius = vals[21]
-            buf, rays = _render(gpu, fz["w"], fz["h"], fz["frames"], fz["max_depth"], camera=cam, flags=V3)
+            buf, rays = _render(gpu, fz["w"], fz["h"], fz["frames"], fz["max_depth"], camera=cam, flags=kflags)
             _assert_bitwise(buf, images[fz["name"]], "v3 " + fz["name"])
             assert rays == fz["rays"], fz["name"]
         gpu.set_scene(*gpu.random_scene(1000, 1))
         for name in ("scene1000_c4_crop", "scene1000_c5_crop"):
             fx = manifest["fixtures"][name]
             buf, rays = _render(gpu, fx["w"], fx["h"], fx["frames"], fx["max_depth"], 0, fx["x0"], fx["xc"],
-                                fx["y0"], fx["yc"], flags=V3)
+                                fx["y0"], fx["yc"], flags=kflags)
             _assert_bitwise(buf, images[name], "v3 " + name)
             assert rays == fx["rays"]
     finally:
         gpu.set_scene(*gpu.default_scene())
 
 
-def test_v3_row_block_cyclic_shard(gpu):
+@ALT
+def test_v3_row_block_cyclic_shard(gpu, kflags):
     """A v3 shard (rows dealt in blocks of 8 over 3 ranks, rank 1) equals the oracle's rows."""
     w, h, rb, period, phase = 320, 180, 8, 3, 1
     rows = [y for y in range(h) if (y // rb) % period == phase]
     job = gpu.Job(width=w, height=h, frames=2, max_depth=8, row_block=rb, row_period=period, row_phase=phase,
-                  flags=V3)
+                  flags=kflags)
     buf = np.zeros((len(rows), w, 4), np.float32)
     rays = gpu.render_host(job, buf)
     want, wrays = oracle.orc_render(w, h, 2, 8)
