@@ -32,10 +32,11 @@ def _job(gpu, w, h, frames, depth, frame0=0, flags=0, x0=0, xc=None, y0=0, yc=No
                    row_count=yc, flags=flags)
 
 
+@pytest.mark.parametrize("kernel", [0, 128, 256], ids=["v0", "v3", "wavefront"])
 @pytest.mark.parametrize("w,h,frames,depth", [(160, 90, 4, 8), (96, 54, 2, 50), (128, 72, 3, 20)])
-def test_no_double_light_vs_oracle(gpu, w, h, frames, depth):
+def test_no_double_light_vs_oracle(gpu, w, h, frames, depth, kernel):
     buf = np.zeros((h, w, 4), np.float32)
-    rays = gpu.render_host(_job(gpu, w, h, frames, depth, flags=64), buf)
+    rays = gpu.render_host(_job(gpu, w, h, frames, depth, flags=64 | kernel), buf)
     want, wr = oracle.orc_render_ex(w, h, frames=frames, depth=depth, flags=64)
     _bitwise(buf, want, "no-double-light")
     assert rays == wr
