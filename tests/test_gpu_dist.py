@@ -1,0 +1,90 @@
+"""The N>1 path on the GPU box with two ranks sharing GPU 0 over gloo (RCCL refuses two
+ranks on one device, so the RCCL gather itself runs only in the driver's multi-GPU
+bench): each rank renders its row-block-cyclic shard with the HIP kernels, the shards go
+to rank 0 through learnraytracing_amd.dist.gather_to_root, rank 0 assembles them with the
+unshard kernel, and the frame equals a one-rank render bit for bit. Also runs bench.py's
+multi-rank path end to end."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, w, h, rb, frames, depth, outdir):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    import learnraytracing_amd as lrt
+    from learnraytracing_amd.dist import gather_to_root, max_shard_rows
+    from learnraytracing_amd.renderer import unshard_tensor
+    lrt.InitializeTest()
+    try:
+        max_rows = max_shard_rows(h, rb, world)
+        local = torch.zeros((max_rows, w, 4), dtype=torch.float32, device="cuda")
+        rays = torch.zeros(1, dtype=torch.int64, device="cuda")
+        job = lrt.Job(width=w, height=h, frames=frames, max_depth=depth, row_block=rb, row_period=world,
+                      row_phase=rank)
+        lrt.render_tensor(job, local, rays)
+        torch.cuda.synchronize()
+        gathered, _ = gather_to_root(local, max_rows, world, rank)
+        tot = rays.cpu()
+        dist.all_reduce(tot)
+        if rank == 0:
+            frame = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
+            unshard_tensor(gathered, frame, w, h, rb, world)
+            torch.cuda.synchronize()
+            np.save(os.path.join(outdir, "frame.npy"), frame.cpu().numpy())
+            np.save(os.path.join(outdir, "rays.npy"), tot.numpy())
+    finally:
+        lrt.ShutdownTest()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,rb,frames", [(2, 8, 4), (2, 5, 32)])
+def test_two_rank_gpu_shards_assemble_bitwise(gpu, tmp_path, world, rb, frames):
+    import torch.multiprocessing as mp
+    w, h, depth = 256, 144, 8
+    mp.start_processes(_worker, args=(world, _free_port(), w, h, rb, frames, depth, str(tmp_path)),
+                       nprocs=world, start_method="spawn", join=True)
+    frame = np.load(tmp_path / "frame.npy")
+    want = np.zeros((h, w, 4), np.float32)
+    want_rays = gpu.render_host(gpu.Job(width=w, height=h, frames=frames, max_depth=depth), want)
+    assert np.array_equal(frame[..., :3].view(np.uint32), want[..., :3].view(np.uint32))
+    assert int(np.load(tmp_path / "rays.npy")[0]) == want_rays
+
+
+def test_bench_two_ranks_gloo(gpu):
+    """bench.py --gpus 2 over gloo on one GPU: one JSON line from rank 0 with the
+    aggregate of both ranks (weak scaling: 8 spp over the two row shards)."""
+    env = dict(os.environ, LRT_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["cpu_baseline"] is None
+    assert d["config"]["spp_total"] == 8
+    assert 2.0e7 < d["config"]["rays_per_step"] < 2.6e7   # ~2 x config 2's 11.67 M rays
+    assert d["value"] > 0
