@@ -53,8 +53,16 @@ LRT_DEV void SlabTest(const float4& mn, const float4& mx, const F3& o, const F3&
 
 struct BvhStats { int nodes = 0, spheres = 0; };   // host diagnostics (lrt_bvh_stats)
 
+// LRT_BVH4 (default): the BVH2 collapsed to 4-wide nodes (8 float4: four children's boxes,
+// same per-child encoding; empty slots have count -1). Half the levels, so fewer and
+// fuller traversal iterations. A stack entry is (node << 4 | mask of the node's children
+// still to visit): one entry per level, re-tested with the tighter bestT when popped.
+#ifndef LRT_BVH4
+#define LRT_BVH4 1
+#endif
+
 // stk: this lane's traversal stack (kBvhStackLevels entries, stride `stride`).
-LRT_DEV int ClosestHitBVH(const F3& o, const F3& d, const BvhView& bv, float& tOut, unsigned short* stk,
+LRT_DEV int ClosestHitBVH2(const F3& o, const F3& d, const BvhView& bv, float& tOut, unsigned short* stk,
                           int stride, BvhStats* st = nullptr) {
     const F3 inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     float bestT = kMaxT;
@@ -136,7 +144,7 @@ LRT_DEV float SphereCand(const F3& o, const F3& d, const float4& s) {   // maths
     const float t2 = rsProj + halfCut;
     return t1 > kMinT ? t1 : (t2 > kMinT ? t2 : __builtin_inff());
 }
-LRT_DEV bool ShadowReachesLightBVH(const F3& o, const F3& d, int li, const float4& lightSph, const BvhView& bv,
+LRT_DEV bool ShadowReachesLightBVH2(const F3& o, const F3& d, int li, const float4& lightSph, const BvhView& bv,
                                    unsigned short* stk, int stride) {
     const float candL = SphereCand(o, d, lightSph);
     if (!(candL < kMaxT)) return false;   // the light is not hit at all (closestT starts at kMaxT)
@@ -185,6 +193,150 @@ LRT_DEV bool ShadowReachesLightBVH(const F3& o, const F3& d, int li, const float
         }
     }
     return true;
+}
+
+
+// 4-wide ClosestHitBVH: same leaf arithmetic, (cand, id) minimum and conservative culling.
+LRT_DEV int ClosestHitBVH4(const F3& o, const F3& d, const BvhView& bv, float& tOut, unsigned short* stk, int stride,
+                           BvhStats* st = nullptr) {
+    const F3 inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    float bestT = kMaxT;
+    int best = -1;
+    auto leaf = [&](int ref, int cnt) {
+        if (st) st->spheres += cnt;
+        for (int j = 0; j < cnt; ++j) {
+            const float4 s = bv.lsph[ref + j];
+            const F3 rs = f3(s.x, s.y, s.z) - o;                       // maths.cpp:54-59
+            const float rsProj = dot(rs, d);
+            const float ifHit = dot(rs, rs) - rsProj * rsProj - s.w;
+            if (ifHit < 0.0f) {
+                const float halfCut = sqrt_rn(-ifHit);
+                const float t1 = rsProj - halfCut;
+                const float t2 = rsProj + halfCut;
+                const float cand = t1 > kMinT ? t1 : (t2 > kMinT ? t2 : __builtin_inff());
+                const int id = bv.lid[ref + j];
+                if (cand < bestT || (cand == bestT && best >= 0 && id < best)) {
+                    bestT = cand;
+                    best = id;
+                }
+            }
+        }
+    };
+    leaf(bv.big0, bv.nbig);
+    if (bv.nnodes == 0) {
+        tOut = bestT;
+        return best;
+    }
+    int sp = 0, cur = 0, msk = 0xF;
+    for (;;) {
+        if (st) st->nodes += 1;
+        const float mb = bv.margin + 1e-5f * bestT;
+        int next = -1, rem = 0;
+        float nearT = __builtin_inff();
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (!((msk >> c) & 1)) continue;
+            const float4 lo = bv.nodes[8 * cur + 2 * c], hi = bv.nodes[8 * cur + 2 * c + 1];
+            const int cnt = lrt::libm::f2u_i(hi.w);
+            if (cnt < 0) continue;
+            float tn, tf;
+            SlabTest(lo, hi, o, inv, tn, tf);
+            const float m = bv.margin + 1e-5f * __builtin_fabsf(tf);
+            if (!(tn <= tf + m && tn <= bestT + mb && tf >= kMinT - m)) continue;
+            if (cnt > 0) {
+                leaf(lrt::libm::f2u_i(lo.w), cnt);
+            } else {
+                rem |= 1 << c;
+                if (tn < nearT) {
+                    nearT = tn;
+                    next = c;
+                }
+            }
+        }
+        if (next >= 0) {
+            rem &= ~(1 << next);
+            if (rem) {
+                stk[sp * stride] = (unsigned short)((cur << 4) | rem);
+                ++sp;
+            }
+            cur = lrt::libm::f2u_i(bv.nodes[8 * cur + 2 * next].w);
+            msk = 0xF;
+        } else {
+            if (sp == 0) break;
+            --sp;
+            const int e = stk[sp * stride];
+            cur = e >> 4;
+            msk = e & 0xF;
+        }
+    }
+    tOut = bestT;
+    return best;
+}
+
+LRT_DEV bool ShadowReachesLightBVH4(const F3& o, const F3& d, int li, const float4& lightSph, const BvhView& bv,
+                                    unsigned short* stk, int stride) {
+    const float candL = SphereCand(o, d, lightSph);
+    if (!(candL < kMaxT)) return false;   // the light is not hit at all (closestT starts at kMaxT)
+    auto beats = [&](float c, int id) { return c < candL || (c == candL && id < li); };
+    for (int j = 0; j < bv.nbig; ++j)
+        if (beats(SphereCand(o, d, bv.lsph[bv.big0 + j]), bv.lid[bv.big0 + j])) return false;
+    if (bv.nnodes == 0) return true;
+    const F3 inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const float mb = bv.margin + 1e-5f * candL;
+    int sp = 0, cur = 0, msk = 0xF;
+    for (;;) {
+        int next = -1, rem = 0;
+        float nearT = __builtin_inff();
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (!((msk >> c) & 1)) continue;
+            const float4 lo = bv.nodes[8 * cur + 2 * c], hi = bv.nodes[8 * cur + 2 * c + 1];
+            const int cnt = lrt::libm::f2u_i(hi.w);
+            if (cnt < 0) continue;
+            float tn, tf;
+            SlabTest(lo, hi, o, inv, tn, tf);
+            const float m = bv.margin + 1e-5f * __builtin_fabsf(tf);
+            if (!(tn <= tf + m && tn <= candL + mb && tf >= kMinT - m)) continue;
+            if (cnt > 0) {
+                const int ref = lrt::libm::f2u_i(lo.w);
+                for (int j = 0; j < cnt; ++j)
+                    if (beats(SphereCand(o, d, bv.lsph[ref + j]), bv.lid[ref + j])) return false;
+            } else {
+                rem |= 1 << c;
+                if (tn < nearT) {
+                    nearT = tn;
+                    next = c;
+                }
+            }
+        }
+        if (next >= 0) {
+            rem &= ~(1 << next);
+            if (rem) {
+                stk[sp * stride] = (unsigned short)((cur << 4) | rem);
+                ++sp;
+            }
+            cur = lrt::libm::f2u_i(bv.nodes[8 * cur + 2 * next].w);
+            msk = 0xF;
+        } else {
+            if (sp == 0) break;
+            --sp;
+            const int e = stk[sp * stride];
+            cur = e >> 4;
+            msk = e & 0xF;
+        }
+    }
+    return true;
+}
+
+// The layout the host built (build_bvh_host): 4-wide unless LRT_BVH4=0.
+LRT_DEV int ClosestHitBVH(const F3& o, const F3& d, const BvhView& bv, float& tOut, unsigned short* stk, int stride,
+                          BvhStats* st = nullptr) {
+    return LRT_BVH4 ? ClosestHitBVH4(o, d, bv, tOut, stk, stride, st) : ClosestHitBVH2(o, d, bv, tOut, stk, stride, st);
+}
+LRT_DEV bool ShadowReachesLightBVH(const F3& o, const F3& d, int li, const float4& lightSph, const BvhView& bv,
+                                   unsigned short* stk, int stride) {
+    return LRT_BVH4 ? ShadowReachesLightBVH4(o, d, li, lightSph, bv, stk, stride)
+                    : ShadowReachesLightBVH2(o, d, li, lightSph, bv, stk, stride);
 }
 
 }  // namespace lrt

@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <functional>
 #include <type_traits>
 #include <cmath>
 #include <mutex>
@@ -640,11 +641,56 @@ void build_bvh_host(const lrt_sphere* s, int n, const std::vector<float4>& sph, 
         B.lid.push_back(i);
     }
     out.nbig = (int)big.size();
+    out.stack_levels = B.max_depth + 1;
+#if LRT_BVH4
+    if (!B.nodes.empty()) {   // collapse the BVH2 into 4-wide nodes (grandchildren of each node)
+        auto ival = [](float f) { int v; memcpy(&v, &f, 4); return v; };
+        auto fval = [](int v) { float f; memcpy(&f, &v, 4); return f; };
+        std::vector<float4> n4;
+        int depth4 = 0;
+        std::function<int(int, int)> collapse = [&](int n2, int dep) -> int {
+            depth4 = std::max(depth4, dep);
+            const int idx = (int)(n4.size() / 8);
+            n4.resize(n4.size() + 8);
+            float4 kids[4][2];
+            int k = 0;
+            for (int c = 0; c < 2; ++c) {
+                const float4 lo = B.nodes[4 * n2 + 2 * c], hi = B.nodes[4 * n2 + 2 * c + 1];
+                if (ival(hi.w) == 0) {   // internal child: take its two children
+                    const int m = ival(lo.w);
+                    for (int g = 0; g < 2; ++g) {
+                        kids[k][0] = B.nodes[4 * m + 2 * g];
+                        kids[k][1] = B.nodes[4 * m + 2 * g + 1];
+                        ++k;
+                    }
+                } else {                 // leaf or empty child stays
+                    kids[k][0] = lo;
+                    kids[k][1] = hi;
+                    ++k;
+                }
+            }
+            for (int c = 0; c < k; ++c)
+                if (ival(kids[c][1].w) == 0) kids[c][0].w = fval(collapse(ival(kids[c][0].w), dep + 1));
+            for (int c = 0; c < 4; ++c) {
+                if (c < k) {
+                    n4[8 * idx + 2 * c] = kids[c][0];
+                    n4[8 * idx + 2 * c + 1] = kids[c][1];
+                } else {   // empty slot
+                    n4[8 * idx + 2 * c] = make_float4(INFINITY, INFINITY, INFINITY, fval(0));
+                    n4[8 * idx + 2 * c + 1] = make_float4(-INFINITY, -INFINITY, -INFINITY, fval(-1));
+                }
+            }
+            return idx;
+        };
+        collapse(0, 0);
+        B.nodes.swap(n4);
+        out.stack_levels = depth4 + 1;   // one (node, child mask) entry per level
+    }
+#endif
     out.nodes.swap(B.nodes);
     out.lsph.swap(B.lsph);
     out.lid.swap(B.lid);
     out.margin = 1e-5f * extent + 1e-4f;
-    out.stack_levels = B.max_depth + 1;
 }
 
 void free_scene(Context& c) {
@@ -701,7 +747,7 @@ int upload_scene(Context& c, const lrt_sphere* s, const lrt_material* m, int n) 
             LRT_HIP(hipMemcpy(c.d_bvh_nodes, B.nodes.data(), sizeof(float4) * B.nodes.size(), hipMemcpyHostToDevice));
         LRT_HIP(hipMemcpy(c.d_bvh_lsph, B.lsph.data(), sizeof(float4) * B.lsph.size(), hipMemcpyHostToDevice));
         LRT_HIP(hipMemcpy(c.d_bvh_lid, B.lid.data(), sizeof(int) * B.lid.size(), hipMemcpyHostToDevice));
-        c.bvh_nodes = (int)(B.nodes.size() / 4);
+        c.bvh_nodes = (int)(B.nodes.size() / (LRT_BVH4 ? 8 : 4));
         c.bvh_big0 = B.big0;
         c.bvh_nbig = B.nbig;
         c.bvh_margin = B.margin;
@@ -1632,7 +1678,7 @@ int lrt_bvh_stats(const lrt_sphere* spheres, int count, const float* rays, int n
     bv.lid = H.lid.data();
     bv.margin = H.margin;
     bv.on = 1;
-    bv.nnodes = (int)(H.nodes.size() / 4);
+    bv.nnodes = (int)(H.nodes.size() / (LRT_BVH4 ? 8 : 4));
     bv.big0 = H.big0;
     bv.nbig = H.nbig;
     double sn = 0, ss = 0, mn = 0, ms = 0, bad = 0;
