@@ -1,11 +1,13 @@
 // liblrt_hip.so — the MI355X path tracer behind the C-ABI of include/lrt.h.
 //
-// One work-item per pixel (TraceRowJob's per-pixel body, parallel.cpp:270-286), all
-// S samples of a pixel inside the work-item (so the progressive lerp sequence of S
-// DrawTest calls is reproduced bit for bit from the buffer's prev value), 16x16-pixel
-// workgroups made of four 8x8 wave tiles (neighbouring pixels take similar paths),
-// the sphere table staged into LDS once per workgroup, RGBA written back with one
-// 16-byte store per pixel, rays counted per lane and reduced once per wave.
+// v0 (trace_kernel, the default): TraceRowJob's per-pixel body (parallel.cpp:270-286)
+// with a pixel's S samples spread over up to 16 adjacent lanes and lerped in frame order
+// (so the progressive sequence of S DrawTest calls is reproduced bit for bit from the
+// buffer's prev value); persistent single-wave workgroups fed from 16 tile queues; the
+// scene, the powf tables and the recursion stack in LDS; one read and one 16-byte write
+// of each pixel per call; rays counted per lane, reduced per wave, folded per queue.
+// Opt-in variants: v1/v2 (lrt_paths*.h), v3 regeneration (lrt_regen.h), v4 wavefront
+// (lrt_wavefront.h). Host side: scene upload + BVH build, launch policy, the C-ABI.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
