@@ -138,6 +138,7 @@ def main():
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--row-block", type=int, default=8)
     ap.add_argument("--spp", type=int, default=None, help="diagnostic: override the config's spp per GPU")
+    ap.add_argument("--depth", type=int, default=None, help="diagnostic: override the config's bounce budget")
     ap.add_argument("--shard-of", type=int, default=1,
                     help="diagnostic (1 process): render only rank 0's shard of an N-GPU weak-scaling run, "
                          "no gather -- the per-GPU render time at N GPUs, measured on one")
@@ -160,6 +161,8 @@ def main():
     cfg = dict(CONFIGS[args.config])
     if args.spp:
         cfg["spp"] = args.spp
+    if args.depth is not None:
+        cfg["depth"] = args.depth
     cfg_name = f"config{args.config}"
 
     # CPU baseline first: rank 0 at N=1 only, before anything touches the GPU.

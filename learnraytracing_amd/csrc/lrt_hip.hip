@@ -1315,7 +1315,6 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     if (kflags & LRT_F_WAVEFRONT) return launch_wavefront(a, lds, s);
     if (kflags & LRT_F_V3) {
         if (d->max_depth <= 8) return launch_regen_split<8>(a, lds, d->x_count, d->row_count, d->frames, s);
-        if (d->max_depth <= 20) return launch_regen_split<20>(a, lds, d->x_count, d->row_count, d->frames, s);
         return launch_regen_split<64>(a, lds, d->x_count, d->row_count, d->frames, s);
     }
     if (!(kflags & LRT_F_SIMPLE)) {
@@ -1366,7 +1365,8 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
         return lds_scene ? launch_paths<true, false, true>(p, s) : launch_paths<false, false, true>(p, s);   // v1
     }
     if (d->max_depth <= 8) return launch_split<8>(a, lds, d->x_count, d->row_count, d->frames, want_feat, s);
-    if (d->max_depth <= 20) return launch_split<20>(a, lds, d->x_count, d->row_count, d->frames, want_feat, s);
+    // depth 9..64: one instance (MAXD only decides whether stack levels beyond the 8 in LDS
+    // exist; 20 and 64 compiled to the same code)
     return launch_split<64>(a, lds, d->x_count, d->row_count, d->frames, want_feat, s);
 }
 
