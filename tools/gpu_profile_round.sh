@@ -10,6 +10,7 @@ run() { local name=$1 t=$2; shift 2; timeout -k 10 $t "$@" > $out/$name.log 2>&1
 run bench 300 python bench.py --steps 20 --warmup 3 $BENCH_ARGS
 tail -1 $out/bench.log > $out/bench.json
 run trace 300 rocprofv3 --kernel-trace --stats -d $out -o trace --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline $BENCH_ARGS
+run trace1 300 rocprofv3 --kernel-trace --stats -d $out -o trace1 --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --streams 1 $BENCH_ARGS
 run fetch 300 rocprofv3 --pmc FETCH_SIZE -d $out -o pmc_fetch --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline $BENCH_ARGS
 run write 300 rocprofv3 --pmc WRITE_SIZE -d $out -o pmc_write --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline $BENCH_ARGS
 run sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_ANY -d $out -o pmc_sq --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline $BENCH_ARGS

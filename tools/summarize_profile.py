@@ -37,13 +37,18 @@ def main():
     key = sys.argv[sys.argv.index("--traffic-key") + 1] if "--traffic-key" in sys.argv else None
     os.makedirs(out, exist_ok=True)
     summary = {"kernel": KERNEL}
-    stats = glob.glob(os.path.join(prof, "*kernel_stats.csv"))
-    for f in stats:
+    # trace_*: the bench's default command (consecutive launches overlap on 2 streams);
+    # trace1_*: the same with --streams 1, each launch alone -- its duration prices the
+    # VALU issue rate of the PMC passes (counter collection serialises launches too)
+    for name, field in (("trace_kernel_stats.csv", "kernel_trace"), ("trace1_kernel_stats.csv", "kernel_trace_serial")):
+        f = os.path.join(prof, name)
+        if not os.path.exists(f):
+            continue
         for r in csv.DictReader(open(f)):
             if KERNEL in r["Name"]:
-                summary["kernel_trace"] = {"name": r["Name"], "calls": int(r["Calls"]),
-                                           "avg_ns": float(r["AverageNs"]), "min_ns": float(r["MinNs"]),
-                                           "max_ns": float(r["MaxNs"]), "percent": float(r["Percentage"])}
+                summary[field] = {"name": r["Name"], "calls": int(r["Calls"]),
+                                  "avg_ns": float(r["AverageNs"]), "min_ns": float(r["MinNs"]),
+                                  "max_ns": float(r["MaxNs"]), "percent": float(r["Percentage"])}
     counters, n, meta = per_launch(os.path.join(prof, "pmc_*counter_collection.csv"))
     summary["launch"] = meta
     summary["counters_per_launch"] = counters
@@ -61,8 +66,9 @@ def main():
             json.dump(d, open(p, "w"), indent=1)
     if "SQ_INSTS_VALU" in counters and "SQ_WAVES" in counters:
         summary["valu_wave_instructions_per_wave"] = counters["SQ_INSTS_VALU"] / counters["SQ_WAVES"]
-        if "kernel_trace" in summary:
-            t = summary["kernel_trace"]["avg_ns"] * 1e-9
+        kt = summary.get("kernel_trace_serial") or summary.get("kernel_trace")
+        if kt:
+            t = kt["avg_ns"] * 1e-9
             # 256 CUs x 4 SIMD, one wave64 VALU instruction per 2 cycles per SIMD at 2.4 GHz
             peak = 256 * 4 * 2.4e9 / 2
             summary["valu_issue_rate"] = counters["SQ_INSTS_VALU"] / t
