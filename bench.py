@@ -121,6 +121,7 @@ def read_valu(cfg_name: str):
             s = json.load(f)
         c = s["counters_per_launch"]
         return {"issue_frac": round(s["valu_issue_frac_of_peak"], 4),
+                "valu_insts_per_launch": c["SQ_INSTS_VALU"],
                 "lane_util": round(c["SQ_THREAD_CYCLES_VALU"] / (c["SQ_ACTIVE_INST_VALU"] * 64), 4),
                 "note": "wave64 VALU instructions issued / (1024 SIMDs x 1 per 2 cycles at 2.4 GHz); "
                         "lane_util = active lanes per VALU instruction / 64",
@@ -302,6 +303,10 @@ def main():
         alg_bytes = BYTES_PER_PIXEL_SAMPLE * pix_samples
         achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
         traffic, traffic_src = read_traffic(f"{cfg_name}_n{world}")
+        valu = read_valu(f"{cfg_name}_n{world}")
+        if valu:   # the committed launch's VALU instructions over this run's wall time per launch
+            valu["issue_frac_effective"] = round(valu["valu_insts_per_launch"] / (elapsed / args.steps)
+                                                 / (256 * 4 * 2.4e9 / 2), 4)
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -347,7 +352,7 @@ def main():
                            "includes the overlap; achieved_effective uses the wall time per launch"
                            if nstreams > 1 else ""),
             },
-            "valu": read_valu(f"{cfg_name}_n{world}"),
+            "valu": valu,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
