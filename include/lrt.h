@@ -19,6 +19,7 @@
  */
 #ifndef LRT_H
 #define LRT_H
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -200,6 +201,14 @@ int lrt_render_host_ex(const lrt_render_desc* desc, float* backbuffer, long long
  * CUs. Destroy with lrt_stream_destroy (lrt_shutdown destroys any left). */
 int lrt_stream_create(int reserved_cus, void** stream);
 int lrt_stream_destroy(void* stream);
+
+/* Page-locked host memory for a backbuffer (hipHostMalloc; contents undefined, like the
+ * `new float[]` of main.cpp:40 it replaces). lrt_draw_test / lrt_render_host(_ex without
+ * features) detect such a buffer -- or any other page-locked one -- and render it in place
+ * over PCIe instead of staging it through device memory either side of the kernel
+ * (LRT_HOST_ZEROCOPY=0 turns that off). Free with lrt_host_free. */
+int lrt_host_alloc(size_t bytes, void** out);
+int lrt_host_free(void* p);
 
 /* Number of local rows GPU `phase` owns in a row-block-cyclic split of `height` rows
  * into blocks of row_block rows dealt over `period` GPUs. */

@@ -107,6 +107,8 @@ SIGNATURES = {
     "lrt_render_host_ex": (_i, [_c.POINTER(RenderDesc), _vp, _c.POINTER(_c.c_longlong), _c.POINTER(Features)]),
     "lrt_stream_create": (_i, [_i, _c.POINTER(_vp)]),
     "lrt_stream_destroy": (_i, [_vp]),
+    "lrt_host_alloc": (_i, [_c.c_size_t, _c.POINTER(_vp)]),
+    "lrt_host_free": (_i, [_vp]),
     "lrt_shard_rows": (_i, [_i, _i, _i, _i]),
     "lrt_unshard_rows": (_i, [_vp, _vp, _i, _i, _i, _i, _vp]),
     "lrt_present_bgra8": (_i, [_vp, _vp, _i, _i, _vp]),

@@ -42,12 +42,18 @@ int main(int argc, char** argv) {
         fprintf(stderr, "usage: %s [width height frames [out.ppm|out.pfm]]\n", argv[0]);
         return 2;
     }
-    float* backbuffer = (float*)calloc((size_t)w * h * 4, sizeof(float)); /* main.cpp:40-41 */
-    if (!backbuffer) return 1;
     if (lrt_initialize() != LRT_OK) {
         fprintf(stderr, "lrt_initialize: %s\n", lrt_last_error());
         return 1;
     }
+    /* main.cpp:40-41, page-locked so that lrt_draw_test renders it in place */
+    const size_t bytes = (size_t)w * h * 4 * sizeof(float);
+    float* backbuffer = NULL;
+    if (lrt_host_alloc(bytes, (void**)&backbuffer) != LRT_OK) {
+        fprintf(stderr, "lrt_host_alloc: %s\n", lrt_last_error());
+        return 1;
+    }
+    memset(backbuffer, 0, bytes);
     double total_s = 0.0;
     long long total_rays = 0;
     for (int f = 0; f < frames; ++f) {
@@ -85,7 +91,7 @@ int main(int argc, char** argv) {
             }
         fclose(fp);
     }
+    lrt_host_free(backbuffer);
     lrt_shutdown();
-    free(backbuffer);
     return 0;
 }

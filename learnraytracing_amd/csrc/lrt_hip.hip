@@ -1380,6 +1380,31 @@ int ensure_frame(size_t bytes) {
     return LRT_OK;
 }
 
+// The device address of buf when it is page-locked host memory (hipHostMalloc /
+// hipHostRegister, e.g. a torch pin_memory tensor), else nullptr.
+float* host_pinned(float* buf) {
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, buf) != hipSuccess) {
+        (void)hipGetLastError();   // pageable memory: clear the error so no later check sees it
+        return nullptr;
+    }
+    if (at.type != hipMemoryTypeHost) return nullptr;
+    return at.devicePointer ? (float*)at.devicePointer : buf;
+}
+
+// Page-locked host backbuffers are rendered in place (zero copy): the kernel's 16 B read
+// and 16 B write per pixel cross PCIe inside the launch instead of a staging copy either
+// side of it (DrawTest at 1280x720: 0.66 ms per frame vs 0.77 staged; staging in row chunks
+// on copy streams measured 0.84 ms at 4 chunks -- per-chunk launch tails and cross-stream
+// waits). LRT_HOST_ZEROCOPY=0 stages them like pageable memory.
+bool host_zero_copy() {
+    static const bool on = [] {
+        const char* e = getenv("LRT_HOST_ZEROCOPY");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
 int render_host(const lrt_render_desc* d, float* buf, long long* out_rays, const lrt_features* feat = nullptr) {
     int rc = validate(d);
     if (rc) return rc;
@@ -1388,6 +1413,16 @@ int render_host(const lrt_render_desc* d, float* buf, long long* out_rays, const
     const size_t bytes = (size_t)d->x_count * d->row_count * 4 * sizeof(float);
     if (bytes == 0 || d->frames == 0) {
         if (out_rays) *out_rays = 0;
+        return LRT_OK;
+    }
+    float* const hdev = (!feat && host_zero_copy()) ? host_pinned(buf) : nullptr;
+    if (hdev) {   // zero copy: the kernel reads and writes the caller's pixels over PCIe
+        LRT_HIP(hipMemsetAsync(g_ctx.d_rays, 0, sizeof(unsigned long long), g_ctx.stream));
+        if ((rc = render_device(d, hdev, g_ctx.d_rays, nullptr, g_ctx.stream))) return rc;
+        unsigned long long rays = 0;
+        LRT_HIP(hipMemcpyAsync(&rays, g_ctx.d_rays, sizeof(rays), hipMemcpyDeviceToHost, g_ctx.stream));
+        LRT_HIP(hipStreamSynchronize(g_ctx.stream));
+        if (out_rays) *out_rays = (long long)rays;
         return LRT_OK;
     }
     if ((rc = ensure_frame(bytes))) return rc;
@@ -1611,6 +1646,23 @@ int lrt_stream_create(int reserved_cus, void** out) {
     LRT_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
     g_ctx.masked_streams.emplace_back(st, kept);
     *out = st;
+    return LRT_OK;
+}
+
+int lrt_host_alloc(size_t bytes, void** out) {
+    if (!out) return fail(LRT_E_INVALID, "out is NULL");
+    *out = nullptr;
+    if (bytes == 0) return fail(LRT_E_INVALID, "bytes must be > 0");
+    if (hipHostMalloc(out, bytes, hipHostMallocDefault) != hipSuccess) {
+        *out = nullptr;
+        return fail(LRT_E_NOMEM, "hipHostMalloc failed");
+    }
+    return LRT_OK;
+}
+
+int lrt_host_free(void* p) {
+    if (!p) return LRT_OK;
+    LRT_HIP(hipHostFree(p));
     return LRT_OK;
 }
 

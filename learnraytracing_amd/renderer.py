@@ -109,6 +109,14 @@ class Job:
         return d
 
 
+def pinned_backbuffer(n_floats: int) -> np.ndarray:
+    """A zeroed float32 host array in page-locked memory (a torch pin_memory tensor viewed
+    by numpy; the array keeps the tensor alive). DrawTest / render_host detect such buffers
+    and let the kernel read and write them in place over PCIe (LRT_HOST_ZEROCOPY=0: staged)."""
+    import torch
+    return torch.zeros(int(n_floats), dtype=torch.float32, pin_memory=True).numpy()
+
+
 def render_host(job: Job, backbuffer: np.ndarray) -> int:
     """Render `job` into a host float32 buffer (row_count*x_count*4). Returns rays."""
     d = job.desc()

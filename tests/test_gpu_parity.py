@@ -114,6 +114,52 @@ def test_draw_test_dropin(gpu):
     _assert_bitwise(bb.reshape(h, w, 4), want[..., :3], "DrawTest x3")
 
 
+def test_draw_test_pinned_backbuffer(gpu):
+    """A page-locked backbuffer is rendered in place over PCIe (zero copy): same bits and
+    rays as the oracle, frames 0..2, and the caller's alpha is left as it was."""
+    w, h = 200, 117
+    bb = gpu.pinned_backbuffer(w * h * 4)
+    bb[3::4] = 0.25
+    want = np.zeros((h, w, 4), np.float32)
+    for f in range(3):
+        rays = gpu.DrawTest(0.0, f, w, h, bb)
+        _, wr = oracle.orc_render(w, h, 1, 20, frame0=f, buf=want)
+        assert rays == wr
+    _assert_bitwise(bb.reshape(h, w, 4), want[..., :3], "DrawTest pinned x3")
+    assert np.all(bb[3::4] == 0.25)
+
+
+def test_host_alloc_backbuffer(gpu):
+    """lrt_host_alloc (main.cpp:40's `new float[]` made page-locked): DrawTest into it equals
+    DrawTest into pageable memory, bit for bit, rays included."""
+    import ctypes
+    w, h = 96, 54
+    n = w * h * 4
+    p = ctypes.c_void_p()
+    assert gpu.lib().lrt_host_alloc(n * 4, ctypes.byref(p)) == 0 and p.value
+    try:
+        a = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_float)), shape=(n,))
+        a[:] = 0.0
+        b = np.zeros(n, np.float32)
+        for f in range(2):
+            assert gpu.DrawTest(0.0, f, w, h, a) == gpu.DrawTest(0.0, f, w, h, b)
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    finally:
+        assert gpu.lib().lrt_host_free(p) == 0
+
+
+def test_render_host_pinned_window(gpu):
+    """lrt_render_host on a pinned buffer: a window of 37 rows x 90 columns, 6 frames,
+    equals the pageable call bit for bit (and so the one-launch render)."""
+    job = gpu.Job(width=160, height=90, frames=6, max_depth=8, x0=30, x_count=90, y0=40, row_count=37)
+    a = np.zeros(37 * 90 * 4, np.float32)
+    b = gpu.pinned_backbuffer(37 * 90 * 4)
+    ra = gpu.render_host(job, a)
+    rb = gpu.render_host(job, b)
+    assert ra == rb > 0
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
 def test_fused_frames_equal_single_frame_calls(gpu):
     """S samples in one call == S one-sample calls (the progressive lerp chain)."""
     a, ra = _render(gpu, 256, 144, 6, 8)
