@@ -459,3 +459,52 @@ def test_many_frames_sample_mode_vs_oracle(gpu, case):
     want, wrays = oracle.orc_render(w, h, frames, depth, frame0=f0)
     _assert_bitwise(buf, want[..., :3], f"{case}")
     assert rays == wrays
+
+
+EDGE_CASES = {
+    "1x1": (1, 1, 3, 8, 0),
+    "1x37": (1, 37, 2, 8, 0),
+    "37x1": (37, 1, 5, 8, 0),
+    "131x3": (131, 3, 4, 8, 0),
+    "depth0": (64, 36, 2, 0, 0),           # no scatter event: every hit is its own emissive
+    "depth1": (64, 36, 2, 1, 0),
+    "depth64": (48, 27, 2, 64, 0),          # the deepest supported budget
+    "lerp_table_edge": (64, 36, 4, 8, 65534),  # frames 65534..65537 cross the host-divided table
+    "seed_wrap": (64, 36, 2, 8, 3000000),   # f * 26699 wraps uint32 as in the reference seed
+    "frames17": (40, 20, 17, 8, 0),         # a 16-lane split plus one frame
+}
+
+
+@pytest.mark.parametrize("kflags", [0, V3, WF], ids=["auto", "v3", "wavefront"])
+@pytest.mark.parametrize("case", list(EDGE_CASES), ids=list(EDGE_CASES))
+def test_edge_cases_vs_oracle(gpu, case, kflags):
+    """Degenerate sizes, depth budgets 0/1/64, frame numbers at the lerp table's end and
+    past the seed's uint32 wrap, odd frame counts: bits and rays equal the oracle."""
+    w, h, frames, depth, f0 = EDGE_CASES[case]
+    buf, rays = _render(gpu, w, h, frames, depth, frame0=f0, flags=kflags)
+    want, wrays = oracle.orc_render(w, h, frames, depth, frame0=f0)
+    _assert_bitwise(buf, want[..., :3], f"{case} flags={kflags}")
+    assert rays == wrays
+
+
+@pytest.mark.parametrize("f0,frames", [(0, 3), (5, 3), (0, 40)])   # 40: few pixels, many frames
+def test_non_finite_prev_propagates_like_reference(gpu, f0, frames):
+    """The lerp reads prev even at frame 0 (prev * 0 + col, parallel.cpp:282): NaN, +-inf
+    and huge values in the caller's buffer propagate exactly as in the reference. NaNs are
+    compared as NaN (their payload bits are platform-defined)."""
+    w, h = 48, 20
+    rng = np.random.default_rng(7)
+    init = rng.uniform(0, 2, (h, w, 4)).astype(np.float32)
+    specials = np.array([np.nan, np.inf, -np.inf, 3.0e38, -3.0e38, 0.0, -0.0], np.float32)
+    mask = rng.random((h, w, 3)) < 0.3
+    init[..., :3][mask] = rng.choice(specials, int(mask.sum()))
+    got = init.copy()
+    want = init.copy()
+    rays = gpu.render_host(gpu.Job(width=w, height=h, frame0=f0, frames=frames, max_depth=8), got)
+    _, wrays = oracle.orc_render(w, h, frames, 8, frame0=f0, buf=want)
+    assert rays == wrays
+    g, e = got[..., :3], want[..., :3]
+    same = (g.view(np.uint32) == e.view(np.uint32)) | (np.isnan(g) & np.isnan(e))
+    assert same.all(), f"{int((~same).sum())} channels differ"
+    assert np.isnan(g).sum() >= int(np.isnan(init[..., :3]).sum())
+    assert np.array_equal(got[..., 3].view(np.uint32), init[..., 3].view(np.uint32))
