@@ -1396,7 +1396,8 @@ float* host_pinned(float* buf) {
 // and 16 B write per pixel cross PCIe inside the launch instead of a staging copy either
 // side of it (DrawTest at 1280x720: 0.66 ms per frame vs 0.77 staged; staging in row chunks
 // on copy streams measured 0.84 ms at 4 chunks -- per-chunk launch tails and cross-stream
-// waits). LRT_HOST_ZEROCOPY=0 stages them like pageable memory.
+// waits; staging only the previous values and letting the kernel write the host pixels
+// measured 0.64 ms, within noise of this). LRT_HOST_ZEROCOPY=0 stages them like pageable memory.
 bool host_zero_copy() {
     static const bool on = [] {
         const char* e = getenv("LRT_HOST_ZEROCOPY");

@@ -148,12 +148,16 @@ def test_host_alloc_backbuffer(gpu):
         assert gpu.lib().lrt_host_free(p) == 0
 
 
-def test_render_host_pinned_window(gpu):
-    """lrt_render_host on a pinned buffer: a window of 37 rows x 90 columns, 6 frames,
-    equals the pageable call bit for bit (and so the one-launch render)."""
-    job = gpu.Job(width=160, height=90, frames=6, max_depth=8, x0=30, x_count=90, y0=40, row_count=37)
-    a = np.zeros(37 * 90 * 4, np.float32)
+@pytest.mark.parametrize("kflags,frames", [(0, 6), (0, 40), (128, 6)], ids=["v0", "v0-samples", "v3"])
+def test_render_host_pinned_window(gpu, kflags, frames):
+    """lrt_render_host on a pinned buffer: a window of 37 rows x 90 columns equals the
+    pageable call bit for bit (and so the one-launch render), alpha included; v0 (also with
+    many frames, sample mode's merge) and v3 (which stages instead)."""
+    job = gpu.Job(width=160, height=90, frames=frames, max_depth=8, x0=30, x_count=90, y0=40, row_count=37,
+                  flags=kflags)
+    a = np.random.default_rng(3).uniform(0, 1, 37 * 90 * 4).astype(np.float32)
     b = gpu.pinned_backbuffer(37 * 90 * 4)
+    b[:] = a
     ra = gpu.render_host(job, a)
     rb = gpu.render_host(job, b)
     assert ra == rb > 0
