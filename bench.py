@@ -263,7 +263,10 @@ def main():
 
     log(f"rank {rank}/{world}: {cfg_name} {W}x{H} spp_total={spp_total} depth={D} rows={rows} "
         f"row_block={rb} scaling={args.scaling}")
-    for k in range(args.warmup):
+    # at least one warmup step per render stream: a stream's first launch grows the
+    # stream-ordered pool for its per-launch buffers (overflow stack, sample planes)
+    warmup = max(args.warmup, nstreams)
+    for k in range(warmup):
         step(k)
     drain()
     torch.cuda.synchronize()
@@ -276,7 +279,7 @@ def main():
         dist.barrier()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(args.warmup + k, ev[k])
+        step(warmup + k, ev[k])
     drain()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
@@ -313,7 +316,7 @@ def main():
             "unit": "Mray/s",
             "n_gpus": world,
             "steps": args.steps,
-            "warmup": args.warmup,
+            "warmup": warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": args.scaling,
