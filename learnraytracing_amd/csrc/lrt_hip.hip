@@ -521,7 +521,7 @@ const lrt_material kDefaultMats[9] = {
 constexpr int kBvhMinSpheres = 16;
 constexpr int kBvhLeaf = 6;   // leaf size (LRT_BVH_LEAF overrides, 1..16; config 4: 4 -> 350 ms, 6 -> 335, 8 -> 336)
 constexpr int kBvhMaxBuildDepth = 22;   // < kBvhStackLevels
-constexpr int kBvhSahMaxDepth = 12;     // SAH splits above this depth, median splits below
+constexpr int kBvhSahMaxDepth = 12;     // SAH splits above this depth, median splits below (LRT_BVH_SAH_DEPTH)
 
 // ---- BVH build (host): SAH splits, median splits on the longest centroid axis deeper down
 struct BvhPrim {
@@ -536,6 +536,7 @@ struct BvhBuilder {
     int max_depth = 0;   // deepest internal node (root = 0)
     bool sah = true;     // SAH splits (LRT_BVH_SPLIT=median: median of the longest centroid axis)
     int leaf = kBvhLeaf;
+    int sahDepth = kBvhSahMaxDepth;
 
     void sort_axis(int b, int e, int k) {
         std::sort(P.begin() + b, P.begin() + e, [k](const BvhPrim& x, const BvhPrim& y) {
@@ -579,7 +580,7 @@ struct BvhBuilder {
         for (int k = 1; k < 3; ++k)
             if (ch[k] - cl[k] > ch[axis] - cl[axis]) axis = k;
         int mid = begin + n / 2;
-        if (sah && depth < kBvhSahMaxDepth) {
+        if (sah && depth < sahDepth) {
             // surface-area heuristic over every split of the centroid order on each axis
             // (full sweep: scenes are at most a few thousand spheres); only above
             // kBvhSahMaxDepth, so the depth bound of the median split still holds
@@ -669,6 +670,8 @@ void build_bvh_host(const lrt_sphere* s, int n, const std::vector<float4>& sph, 
         B.sah = !(e && strcmp(e, "median") == 0);
         const char* l = getenv("LRT_BVH_LEAF");
         if (l) B.leaf = std::min(16, std::max(1, atoi(l)));
+        const char* sd = getenv("LRT_BVH_SAH_DEPTH");
+        if (sd) B.sahDepth = std::min(kBvhMaxBuildDepth, std::max(0, atoi(sd)));
     }
     float extent = 1.0f;
     for (int i = 0; i < n; ++i) {
