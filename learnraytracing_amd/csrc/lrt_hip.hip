@@ -659,9 +659,15 @@ struct BvhHost {
 void build_bvh_host(const lrt_sphere* s, int n, const std::vector<float4>& sph, BvhHost& out) {
     std::vector<float> radii(n);
     for (int i = 0; i < n; ++i) radii[i] = std::fabs(s[i].radius);
-    std::vector<float> sorted = radii;
-    std::nth_element(sorted.begin(), sorted.begin() + n / 2, sorted.end());
-    const float big_r = 8.0f * sorted[n / 2];
+    std::vector<float> sorted;
+    for (float r : radii)
+        if (std::isfinite(r)) sorted.push_back(r);
+    float big_r = INFINITY;
+    if (!sorted.empty()) {
+        const size_t m = sorted.size() / 2;
+        std::nth_element(sorted.begin(), sorted.begin() + m, sorted.end());
+        big_r = 8.0f * sorted[m];
+    }
     std::vector<int> big;
     BvhBuilder B;
     B.sph = &sph;
@@ -675,7 +681,11 @@ void build_bvh_host(const lrt_sphere* s, int n, const std::vector<float4>& sph, 
     }
     float extent = 1.0f;
     for (int i = 0; i < n; ++i) {
-        if (radii[i] > big_r && big.size() < 16) {
+        const bool finite = std::isfinite(s[i].center.x) && std::isfinite(s[i].center.y) &&
+                            std::isfinite(s[i].center.z) && std::isfinite(radii[i]);
+        // non-finite spheres have no box (and would break the split's ordering): like the
+        // ground they are tested in index order by every ray, as in the reference's scan
+        if (!finite || (radii[i] > big_r && big.size() < 16)) {
             big.push_back(i);
             continue;
         }

@@ -74,3 +74,20 @@ def test_axis_aligned_and_surface_rays():
         nrm /= np.linalg.norm(nrm)
         rays.append(np.concatenate([c + s.radius * nrm, g.normal(size=3)]))
     assert stats(sph, np.array(rays, np.float32))[4] == 0.0
+
+
+@pytest.mark.parametrize("bad", [1, 40])
+def test_non_finite_spheres(bad):
+    """Spheres with NaN / inf centres or radii stay out of the tree and are tested by every
+    ray (the build never orders them), so the result still equals the linear scan."""
+    g = np.random.default_rng(bad)
+    sph, _ = random_scene(300, 2)
+    vals = [float("nan"), float("inf"), -float("inf")]
+    for k, i in enumerate(g.choice(np.arange(1, 300), bad, replace=False)):
+        s = sph[int(i)]
+        if k % 2:
+            s.radius = vals[k % 3]
+        else:
+            s.center = L.f3(vals[k % 3], s.center.y, s.center.z)
+    rays = random_rays(g, 3000, [-6, -0.6, -7], [6, 3, 4])
+    assert stats(sph, rays)[4] == 0.0
