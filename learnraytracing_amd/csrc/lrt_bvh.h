@@ -51,6 +51,51 @@ LRT_DEV void SlabTest(const float4& mn, const float4& mx, const F3& o, const F3&
                          __builtin_fmaxf(tz0, tz1));
 }
 
+// The 4-wide traversals' slab test: t = fma(plane, inv, -o * inv), one FMA per plane
+// instead of a subtract and a multiply. Beyond the subtract-multiply form's rounding it
+// errs by at most ulp(|o_k * inv_k|) per plane; SlabOriginMargin bounds that once per ray
+// and the culling margins add it, so culling stays conservative.
+#ifndef LRT_BVH_FMA_SLAB
+#define LRT_BVH_FMA_SLAB 1
+#endif
+LRT_DEV void SlabTestFma(const float4& mn, const float4& mx, const F3& inv, const F3& oi, float& tn, float& tf) {
+    const float tx0 = __builtin_fmaf(mn.x, inv.x, -oi.x), tx1 = __builtin_fmaf(mx.x, inv.x, -oi.x);
+    const float ty0 = __builtin_fmaf(mn.y, inv.y, -oi.y), ty1 = __builtin_fmaf(mx.y, inv.y, -oi.y);
+    const float tz0 = __builtin_fmaf(mn.z, inv.z, -oi.z), tz1 = __builtin_fmaf(mx.z, inv.z, -oi.z);
+    tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(tx0, tx1), __builtin_fminf(ty0, ty1)),
+                         __builtin_fminf(tz0, tz1));
+    tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(tx0, tx1), __builtin_fmaxf(ty0, ty1)),
+                         __builtin_fmaxf(tz0, tz1));
+}
+// The FMA form is used only when no product can overflow: an infinite inv_k (a direction
+// component of 0) makes plane * inv - o * inv an inf - inf = NaN, which the min/max would
+// resolve to the wrong extreme. Such rays keep the subtract-multiply form. With finite
+// products the extra margin is mo = 2^-22 * max_k |o_k * inv_k|, 4x the bound above.
+struct SlabRay {
+    F3 inv, oi;
+    float mo;
+    bool fma;
+};
+LRT_DEV SlabRay MakeSlabRay(const F3& o, const F3& d, float margin) {
+    SlabRay r;
+    r.inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    r.oi = f3(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
+    const float mi = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.inv.x), __builtin_fabsf(r.inv.y)),
+                                     __builtin_fabsf(r.inv.z));
+    const float mo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(o.x), __builtin_fabsf(o.y)), __builtin_fabsf(o.z));
+    // margin = 1e-5 * extent + 1e-4 (build_bvh_host): every box coordinate is below 1e5 * margin
+    const float bound = mi * (1.0e5f * margin + mo);
+    r.fma = LRT_BVH_FMA_SLAB && bound < 1.0e30f;   // false for inf / NaN too
+    r.mo = r.fma ? __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.oi.x), __builtin_fabsf(r.oi.y)),
+                                   __builtin_fabsf(r.oi.z)) * 2.384185791015625e-07f
+                 : 0.0f;
+    return r;
+}
+LRT_DEV void SlabTest4(const float4& mn, const float4& mx, const F3& o, const SlabRay& sr, float& tn, float& tf) {
+    if (sr.fma) SlabTestFma(mn, mx, sr.inv, sr.oi, tn, tf);
+    else SlabTest(mn, mx, o, sr.inv, tn, tf);
+}
+
 struct BvhStats { int nodes = 0, spheres = 0; };   // host diagnostics (lrt_bvh_stats)
 
 // LRT_BVH4 (default): the BVH2 collapsed to 4-wide nodes (8 float4: four children's boxes,
@@ -199,7 +244,7 @@ LRT_DEV bool ShadowReachesLightBVH2(const F3& o, const F3& d, int li, const floa
 // 4-wide ClosestHitBVH: same leaf arithmetic, (cand, id) minimum and conservative culling.
 LRT_DEV int ClosestHitBVH4(const F3& o, const F3& d, const BvhView& bv, float& tOut, unsigned short* stk, int stride,
                            BvhStats* st = nullptr) {
-    const F3 inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const SlabRay sr = MakeSlabRay(o, d, bv.margin);
     float bestT = kMaxT;
     int best = -1;
     auto leaf = [&](int ref, int cnt) {
@@ -230,7 +275,7 @@ LRT_DEV int ClosestHitBVH4(const F3& o, const F3& d, const BvhView& bv, float& t
     int sp = 0, cur = 0, msk = 0xF;
     for (;;) {
         if (st) st->nodes += 1;
-        const float mb = bv.margin + 1e-5f * bestT;
+        const float mb = bv.margin + sr.mo + 1e-5f * bestT;
         int next = -1, rem = 0;
         float nearT = __builtin_inff();
 #pragma unroll
@@ -240,8 +285,8 @@ LRT_DEV int ClosestHitBVH4(const F3& o, const F3& d, const BvhView& bv, float& t
             const int cnt = lrt::libm::f2u_i(hi.w);
             if (cnt < 0) continue;
             float tn, tf;
-            SlabTest(lo, hi, o, inv, tn, tf);
-            const float m = bv.margin + 1e-5f * __builtin_fabsf(tf);
+            SlabTest4(lo, hi, o, sr, tn, tf);
+            const float m = bv.margin + sr.mo + 1e-5f * __builtin_fabsf(tf);
             if (!(tn <= tf + m && tn <= bestT + mb && tf >= kMinT - m)) continue;
             if (cnt > 0) {
                 leaf(lrt::libm::f2u_i(lo.w), cnt);
@@ -281,8 +326,8 @@ LRT_DEV bool ShadowReachesLightBVH4(const F3& o, const F3& d, int li, const floa
     for (int j = 0; j < bv.nbig; ++j)
         if (beats(SphereCand(o, d, bv.lsph[bv.big0 + j]), bv.lid[bv.big0 + j])) return false;
     if (bv.nnodes == 0) return true;
-    const F3 inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    const float mb = bv.margin + 1e-5f * candL;
+    const SlabRay sr = MakeSlabRay(o, d, bv.margin);
+    const float mb = bv.margin + sr.mo + 1e-5f * candL;
     int sp = 0, cur = 0, msk = 0xF;
     for (;;) {
         int next = -1, rem = 0;
@@ -294,8 +339,8 @@ LRT_DEV bool ShadowReachesLightBVH4(const F3& o, const F3& d, int li, const floa
             const int cnt = lrt::libm::f2u_i(hi.w);
             if (cnt < 0) continue;
             float tn, tf;
-            SlabTest(lo, hi, o, inv, tn, tf);
-            const float m = bv.margin + 1e-5f * __builtin_fabsf(tf);
+            SlabTest4(lo, hi, o, sr, tn, tf);
+            const float m = bv.margin + sr.mo + 1e-5f * __builtin_fabsf(tf);
             if (!(tn <= tf + m && tn <= candL + mb && tf >= kMinT - m)) continue;
             if (cnt > 0) {
                 const int ref = lrt::libm::f2u_i(lo.w);
