@@ -276,6 +276,7 @@ LRT_DEV int ClosestHitBVH4(const F3& o, const F3& d, const BvhView& bv, float& t
     for (;;) {
         if (st) st->nodes += 1;
         const float mb = bv.margin + sr.mo + 1e-5f * bestT;
+        const float mbase = bv.margin + sr.mo;
         int next = -1, rem = 0;
         float nearT = __builtin_inff();
 #pragma unroll
@@ -286,7 +287,7 @@ LRT_DEV int ClosestHitBVH4(const F3& o, const F3& d, const BvhView& bv, float& t
             if (cnt < 0) continue;
             float tn, tf;
             SlabTest4(lo, hi, o, sr, tn, tf);
-            const float m = bv.margin + sr.mo + 1e-5f * __builtin_fabsf(tf);
+            const float m = __builtin_fmaf(1e-5f, __builtin_fabsf(tf), mbase);   // a margin: rounding is immaterial
             if (!(tn <= tf + m && tn <= bestT + mb && tf >= kMinT - m)) continue;
             if (cnt > 0) {
                 leaf(lrt::libm::f2u_i(lo.w), cnt);
@@ -328,6 +329,7 @@ LRT_DEV bool ShadowReachesLightBVH4(const F3& o, const F3& d, int li, const floa
     if (bv.nnodes == 0) return true;
     const SlabRay sr = MakeSlabRay(o, d, bv.margin);
     const float mb = bv.margin + sr.mo + 1e-5f * candL;
+    const float mbase = bv.margin + sr.mo;
     int sp = 0, cur = 0, msk = 0xF;
     for (;;) {
         int next = -1, rem = 0;
@@ -340,7 +342,7 @@ LRT_DEV bool ShadowReachesLightBVH4(const F3& o, const F3& d, int li, const floa
             if (cnt < 0) continue;
             float tn, tf;
             SlabTest4(lo, hi, o, sr, tn, tf);
-            const float m = bv.margin + sr.mo + 1e-5f * __builtin_fabsf(tf);
+            const float m = __builtin_fmaf(1e-5f, __builtin_fabsf(tf), mbase);   // a margin: rounding is immaterial
             if (!(tn <= tf + m && tn <= candL + mb && tf >= kMinT - m)) continue;
             if (cnt > 0) {
                 const int ref = lrt::libm::f2u_i(lo.w);
