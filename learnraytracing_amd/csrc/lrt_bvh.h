@@ -288,7 +288,8 @@ LRT_DEV int ClosestHitBVH4(const F3& o, const F3& d, const BvhView& bv, float& t
             float tn, tf;
             SlabTest4(lo, hi, o, sr, tn, tf);
             const float m = __builtin_fmaf(1e-5f, __builtin_fabsf(tf), mbase);   // a margin: rounding is immaterial
-            if (!(tn <= tf + m && tn <= bestT + mb && tf >= kMinT - m)) continue;
+            const float tfm = tf + m;   // (tn <= tf + m, tn <= bestT + mb, tf + m >= kMinT)
+            if (!(tn <= __builtin_fminf(tfm, bestT + mb) && tfm >= kMinT)) continue;
             if (cnt > 0) {
                 leaf(lrt::libm::f2u_i(lo.w), cnt);
             } else {
@@ -343,7 +344,8 @@ LRT_DEV bool ShadowReachesLightBVH4(const F3& o, const F3& d, int li, const floa
             float tn, tf;
             SlabTest4(lo, hi, o, sr, tn, tf);
             const float m = __builtin_fmaf(1e-5f, __builtin_fabsf(tf), mbase);   // a margin: rounding is immaterial
-            if (!(tn <= tf + m && tn <= candL + mb && tf >= kMinT - m)) continue;
+            const float tfm = tf + m;   // (tn <= tf + m, tn <= candL + mb, tf + m >= kMinT)
+            if (!(tn <= __builtin_fminf(tfm, candL + mb) && tfm >= kMinT)) continue;
             if (cnt > 0) {
                 const int ref = lrt::libm::f2u_i(lo.w);
                 for (int j = 0; j < cnt; ++j)
