@@ -372,6 +372,16 @@ LRT_DEV bool ShadowReachesLightBVH4(const F3& o, const F3& d, int li, const floa
             const int e = stk[sp * stride];
             cur = e >> 4;
             msk = e & 0xF;
+            // candL does not shrink, so the popped children's boxes passed already: descend
+            // into the first without testing again, push the rest back
+            const int c = __builtin_ctz(msk);
+            msk &= msk - 1;
+            if (msk) {
+                stk[sp * stride] = (unsigned short)((cur << 4) | msk);
+                ++sp;
+            }
+            cur = lrt::libm::f2u_i(bv.nodes[8 * cur + 2 * c].w);
+            msk = 0xF;
         }
     }
     return true;
