@@ -55,6 +55,9 @@ LRT_DEV void SlabTest(const float4& mn, const float4& mx, const F3& o, const F3&
 // instead of a subtract and a multiply. Beyond the subtract-multiply form's rounding it
 // errs by at most ulp(|o_k * inv_k|) per plane; SlabOriginMargin bounds that once per ray
 // and the culling margins add it, so culling stays conservative.
+#ifndef LRT_BVH_CH_RETEST   // closest hit: re-test popped children against the shrunk bestT
+#define LRT_BVH_CH_RETEST 0
+#endif
 #ifndef LRT_BVH_FMA_SLAB
 #define LRT_BVH_FMA_SLAB 1
 #endif
@@ -314,6 +317,16 @@ LRT_DEV int ClosestHitBVH4(const F3& o, const F3& d, const BvhView& bv, float& t
             const int e = stk[sp * stride];
             cur = e >> 4;
             msk = e & 0xF;
+#if !LRT_BVH_CH_RETEST
+            const int c = __builtin_ctz(msk);
+            msk &= msk - 1;
+            if (msk) {
+                stk[sp * stride] = (unsigned short)((cur << 4) | msk);
+                ++sp;
+            }
+            cur = lrt::libm::f2u_i(bv.nodes[8 * cur + 2 * c].w);
+            msk = 0xF;
+#endif
         }
     }
     tOut = bestT;
