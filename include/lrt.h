@@ -99,10 +99,9 @@ typedef struct lrt_render_desc {
 #define LRT_F_SIMPLE 2       /* v0 kernel (the default): the reference's per-pixel loop,
                                 a pixel's frames spread over adjacent lanes, persistent
                                 single-wave blocks fed from tile queues               */
-#define LRT_F_V1 4           /* v1 kernel: per-lane state machine without phase
-                                scheduling (for A/B); default is v2                    */
-#define LRT_F_V2S 8          /* v2 phase scheduling with one static pixel per lane for
-                                the whole launch (no work queue)                       */
+#define LRT_F_V1 4           /* removed (round-1 per-lane state machine, always slower
+                                than SIMPLE): rejected with LRT_E_INVALID             */
+#define LRT_F_V2S 8          /* removed, as LRT_F_V1                                   */
 #define LRT_F_NO_BVH 32      /* scan every sphere (the reference's HitWorld loop) even
                                 when the scene has a BVH (> 16 spheres)                */
 #define LRT_F_NO_DOUBLE_LIGHT 64 /* opt-in GL-path rule (fragmentShader.fs.glsl:430,456-457,
@@ -111,9 +110,8 @@ typedef struct lrt_render_desc {
                                 sampled explicitly); the terminating hit always adds it.
                                 Off by default: the CPU reference double counts
                                 (parallel.cpp:214). v0 kernel only.                   */
-#define LRT_F_V2 16          /* v2 persistent mode (work queue: static chunks, then
-                                atomics). With none of SIMPLE/V1/V2S/V2 set the library
-                                runs SIMPLE (fastest on every measured config).        */
+#define LRT_F_V2 16          /* removed, as LRT_F_V1. With none of SIMPLE/V3/WAVEFRONT
+                                set the library runs SIMPLE (fastest on every config). */
 #define LRT_F_V3 128         /* v3 kernel: the v0 loop with path regeneration inside the
                                 wave (a lane traces its pixel's frames in turn; ended
                                 lanes are refilled together from the wave's pixel
@@ -144,6 +142,10 @@ int lrt_draw_test(float time, int frameCount, int screenWidth, int screenHeight,
 const char* lrt_last_error(void);
 /* Library version string ("lrt-mi355x <semver> gfx950"). */
 const char* lrt_version(void);
+/* The kernel instance the last render call on any thread launched, as "key=value" words
+ * (e.g. "kernel=trace_kernel maxd=8 lds=1 bvh=1 split=16 samp=0 feat=0 ns=0 grid=4096
+ * tasks=..."): lets tests and benchmarks name the exact instance they exercised. */
+const char* lrt_last_launch(void);
 
 /* Camera constructor (maths.h:183-202). */
 int lrt_camera_make(lrt_float3 lookFrom, lrt_float3 lookAt, lrt_float3 vup, float vfov,

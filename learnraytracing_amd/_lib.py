@@ -26,11 +26,13 @@ REFERENCE_MAX_DEPTH = 20                      # parallel.cpp:12
 MAX_SPHERES = 4096
 F_SCENE_GLOBAL = 1
 F_SIMPLE = 2
-F_V1 = 4
+F_V1 = 4            # removed kernels: rejected with LRT_E_INVALID
 F_V2S = 8
 F_V2 = 16
 F_NO_BVH = 32
 F_NO_DOUBLE_LIGHT = 64
+F_V3 = 128
+F_WAVEFRONT = 256
 
 
 class LrtError(RuntimeError):
@@ -96,6 +98,7 @@ SIGNATURES = {
     "lrt_draw_test": (_i, [_c.c_float, _i, _i, _i, _vp, _c.POINTER(_i)]),
     "lrt_last_error": (_c.c_char_p, []),
     "lrt_version": (_c.c_char_p, []),
+    "lrt_last_launch": (_c.c_char_p, []),
     "lrt_camera_make": (_i, [Float3, Float3, Float3, _c.c_float, _c.c_float, _c.c_float,
                              _c.c_float, _c.POINTER(Camera)]),
     "lrt_camera_default": (_i, [_i, _i, _c.POINTER(Camera)]),
@@ -148,6 +151,12 @@ def lib() -> ctypes.CDLL:
                 fn.argtypes = args
             _lib = handle
         return _lib
+
+
+def last_launch() -> dict:
+    """The kernel instance of the last render call (lrt_last_launch) as a dict."""
+    words = lib().lrt_last_launch().decode().split()
+    return dict(w.split("=", 1) for w in words if "=" in w)
 
 
 def check(rc: int) -> int:

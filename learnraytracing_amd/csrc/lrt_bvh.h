@@ -22,6 +22,7 @@
 //
 // Included by lrt_trace.h (it uses F3, dot, kMinT, kMaxT defined there).
 #pragma once
+#include "lrt.h"   // LRT_MAX_SPHERES
 
 namespace lrt {
 
@@ -53,11 +54,8 @@ LRT_DEV void SlabTest(const float4& mn, const float4& mx, const F3& o, const F3&
 
 // The 4-wide traversals' slab test: t = fma(plane, inv, -o * inv), one FMA per plane
 // instead of a subtract and a multiply. Beyond the subtract-multiply form's rounding it
-// errs by at most ulp(|o_k * inv_k|) per plane; SlabOriginMargin bounds that once per ray
+// errs by at most ulp(|o_k * inv_k|) per plane; MakeSlabRay bounds that once per ray
 // and the culling margins add it, so culling stays conservative.
-#ifndef LRT_BVH_CH_RETEST   // closest hit: re-test popped children against the shrunk bestT
-#define LRT_BVH_CH_RETEST 0
-#endif
 #ifndef LRT_BVH_FMA_SLAB
 #define LRT_BVH_FMA_SLAB 1
 #endif
@@ -104,10 +102,18 @@ struct BvhStats { int nodes = 0, spheres = 0; };   // host diagnostics (lrt_bvh_
 // LRT_BVH4 (default): the BVH2 collapsed to 4-wide nodes (8 float4: four children's boxes,
 // same per-child encoding; empty slots have count -1). Half the levels, so fewer and
 // fuller traversal iterations. A stack entry is (node << 4 | mask of the node's children
-// still to visit): one entry per level, re-tested with the tighter bestT when popped.
+// still to visit), one entry per level. A popped entry descends into its first child
+// without a second box test: every pushed child already passed the cull against a bound
+// that has only shrunk since, so skipping the re-test is conservative.
 #ifndef LRT_BVH4
 #define LRT_BVH4 1
 #endif
+#ifndef LRT_BVH_CH_RETEST   // closest hit: re-test popped children against the shrunk bestT (A/B)
+#define LRT_BVH_CH_RETEST 0
+#endif
+// A BVH4 stack entry is a u16 (node << 4 | mask): node indices must stay below 4096. The
+// 4-wide node count is at most the BVH2's internal node count, < LRT_MAX_SPHERES.
+static_assert(LRT_MAX_SPHERES <= 4096, "BVH4 stack entries hold 12-bit node indices");
 
 // stk: this lane's traversal stack (kBvhStackLevels entries, stride `stride`).
 LRT_DEV int ClosestHitBVH2(const F3& o, const F3& d, const BvhView& bv, float& tOut, unsigned short* stk,

@@ -6,8 +6,7 @@
 // buffer's prev value); persistent single-wave workgroups fed from 16 tile queues; the
 // scene, the powf tables and the recursion stack in LDS; one read and one 16-byte write
 // of each pixel per call; rays counted per lane, reduced per wave, folded per queue.
-// Opt-in variants: v1/v2 (lrt_paths*.h), v3 regeneration (lrt_regen.h), v4 wavefront
-// (lrt_wavefront.h). Host side: scene upload + BVH build, launch policy, the C-ABI.
+// Opt-in variants: v3 regeneration (lrt_regen.h), v4 wavefront (lrt_wavefront.h). Host side: scene upload + BVH build, launch policy, the C-ABI.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
@@ -22,11 +21,9 @@
 #include <vector>
 
 #include "lrt.h"
-#include "lrt_paths.h"
-#include "lrt_paths2.h"
 #include "lrt_trace.h"
 
-#define LRT_VERSION_STRING "lrt-mi355x 0.1.0 gfx950"
+#define LRT_VERSION_STRING "lrt-mi355x 0.2.0 gfx950"
 
 namespace lrt {
 
@@ -442,7 +439,6 @@ __global__ void libm_kernel(int kind, const float* __restrict__ in, float* __res
 // host side
 constexpr int kQueueSlots = 64;
 constexpr size_t kTileSetU64 = 2 * kV0Queues * kCtrStride;   // one v0 launch's counters
-constexpr int kLdsLevels = 8;
 
 struct Context {
     bool ready = false;
@@ -450,8 +446,6 @@ struct Context {
     int num_cus = 0;
     // render streams created by lrt_stream_create: CU-masked, and the CUs they may use
     std::vector<std::pair<hipStream_t, int>> masked_streams;
-    unsigned int* d_queue = nullptr;   // kQueueSlots work counters, one per in-flight launch
-    unsigned queue_next = 0;
     unsigned long long* d_tiles = nullptr;   // kQueueSlots x v0 counter sets (trace_kernel)
     float* d_lerp = nullptr;                 // kLerpTable lerp factors (host IEEE division)
     struct Wavefront {                       // v4 path state, grown on demand
@@ -485,6 +479,7 @@ struct Context {
 
 Context g_ctx;
 std::mutex g_mu;
+char g_last_launch[256] = "";   // lrt_last_launch(): the kernel instance of the last render call
 thread_local std::string t_err;
 
 int fail(int code, const std::string& msg) {
@@ -995,6 +990,9 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     }
     const long long tasks = samp ? ntiles * rounds : ntiles;
     long long blocks = (long long)per_cu * cus * LRT_V0_GRID_MULT;
+    // block b serves queue b % kV0Queues: every queue that owns a task needs a block, even
+    // on a CU-masked stream left with fewer slots than queues (those blocks start later)
+    blocks = std::max(blocks, (long long)kV0Queues);
     if (blocks > tasks) blocks = tasks;
     const dim3 grid((unsigned)blocks);
     a.samp = nullptr;
@@ -1046,6 +1044,10 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     }
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "trace_kernel launch");
+    snprintf(g_last_launch, sizeof(g_last_launch),
+             "kernel=trace_kernel maxd=%d lds=%d bvh=%d split=%d samp=%d feat=%d ns=%d grid=%u tasks=%lld per_cu=%d",
+             MAXD, lds ? 1 : 0, a.bv.on ? 1 : 0, kSplit, samp ? 1 : 0, kFeat ? 1 : 0, fixed ? kFixedSpheres : 0,
+             grid.x, tasks, per_cu);
 
 #ifdef LRT_EXP_WAVETRACE
     wavetrace_dump(a.wtrace, (size_t)grid.x * (kBlock / 64), s);
@@ -1102,7 +1104,7 @@ int launch_regen(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     int cus = g_ctx.num_cus;
     for (const auto& m : g_ctx.masked_streams)
         if (m.first == s) cus = m.second;
-    long long blocks = (long long)per_cu * cus;
+    long long blocks = std::max((long long)per_cu * cus, (long long)kV0Queues);   // a block per queue (as v0)
     if (blocks > ntiles) blocks = ntiles;
     const dim3 grid((unsigned)blocks);
     a.ovf = nullptr;
@@ -1134,6 +1136,8 @@ int launch_regen(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     }
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "regen_kernel launch");
+    snprintf(g_last_launch, sizeof(g_last_launch), "kernel=regen_kernel maxd=%d lds=%d bvh=%d split=%d grid=%u tasks=%lld",
+             MAXD, lds ? 1 : 0, a.bv.on ? 1 : 0, kSplit, grid.x, ntiles);
 
 #ifdef LRT_EXP_SECSTATS
     secstats_dump(d_sec, s);
@@ -1242,71 +1246,10 @@ int launch_wavefront(KernelArgs a, bool lds, hipStream_t s) {
         e = hipGetLastError();
         if (e != hipSuccess) return hip_fail(e, "wavefront launch");
     }
+    snprintf(g_last_launch, sizeof(g_last_launch), "kernel=wf_extend lds=%d bvh=%d grid=%u", lds ? 1 : 0, bvh ? 1 : 0, grid.x);
     wf_rays_collect<<<1, 64, 0, s>>>(wf.rayp, a.rays);
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "wavefront ray collect");
-    return LRT_OK;
-}
-
-template <bool kLdsScene, bool kV2, bool kOverflow, int kPix = 0, bool kBvh = false>
-int launch_paths(PathArgs& a, hipStream_t s) {
-    constexpr bool kStaticPixel = kPix > 0;
-    const size_t lds = paths_lds_bytes(kLdsLevels, kLdsScene, a.count, a.nlights, kPix, a.bv.on != 0);
-    a.bvh_stack_offset = (int)paths_lds_bytes(kLdsLevels, kLdsScene, a.count, a.nlights, kPix, false);
-    int per_cu = 0;
-    const void* kern = kV2 ? (const void*)paths2_kernel<kLdsLevels, kLdsScene, kOverflow, kPix, kBvh>
-                           : (const void*)paths_kernel<kLdsLevels, kLdsScene>;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kPathBlock, lds);
-    if (e != hipSuccess) return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
-    if (per_cu < 1) return fail(LRT_E_INVALID, "paths_kernel does not fit on a CU (scene too large for LDS)");
-    long long want = ((long long)a.nitems + kPathBlock - 1) / kPathBlock;
-    long long blocks = (long long)per_cu * g_ctx.num_cus;
-    if (blocks > want) blocks = want;
-    dim3 grid((unsigned)blocks);
-    if constexpr (kStaticPixel) {   // kPix pixels per lane: 16 x 16*kPix tiles, no persistence
-        grid = dim3((unsigned)((a.xc + 15) / 16), (unsigned)((a.rows + 16 * kPix - 1) / (16 * kPix)));
-        blocks = (long long)grid.x * grid.y;
-    }
-    const size_t gthreads = (size_t)blocks * kPathBlock;   // = gridDim.x * gridDim.y * kPathBlock
-    float4* overflow = nullptr;
-    if (a.maxDepth > kLdsLevels) {
-        e = hipMallocAsync((void**)&overflow, sizeof(float4) * gthreads * (size_t)(a.maxDepth - kLdsLevels), s);
-        if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(path stack overflow)");
-    }
-    a.overflow = overflow;
-    a.stamps = nullptr;
-#ifdef LRT_EXP_STAMPS
-    static unsigned long long* d_stamps = nullptr;
-    if (!d_stamps) (void)hipMalloc(&d_stamps, sizeof(unsigned long long) * 3 * (kSecCount + 1));
-    (void)hipMemsetAsync(d_stamps, 0, sizeof(unsigned long long) * 3 * (kSecCount + 1), s);
-    a.stamps = d_stamps;
-#endif
-    unsigned int* q = g_ctx.d_queue + (g_ctx.queue_next++ % kQueueSlots);
-    a.queue = q;
-    e = hipMemsetAsync(q, 0, sizeof(unsigned int), s);
-    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(queue)");
-    if (kV2)
-        paths2_kernel<kLdsLevels, kLdsScene, kOverflow, kPix, kBvh><<<grid, kPathBlock, lds, s>>>(a);
-    else
-        paths_kernel<kLdsLevels, kLdsScene><<<dim3((unsigned)blocks), kPathBlock, lds, s>>>(a);
-    e = hipGetLastError();
-    if (e != hipSuccess) return hip_fail(e, "paths_kernel launch");
-#ifdef LRT_EXP_STAMPS
-    {
-        unsigned long long h[3 * (kSecCount + 1)];
-        (void)hipMemcpyAsync(h, d_stamps, sizeof(h), hipMemcpyDeviceToHost, s);
-        (void)hipStreamSynchronize(s);
-        const char* names[] = {"trace", "light", "spec", "camera", "sched"};
-        for (int i = 0; i <= kSecCount; ++i)
-            fprintf(stderr, "stamps %-8s cycles %14llu  execs %10llu  lanes/exec %6.2f  cyc/exec %8.1f\n", names[i],
-                    h[3 * i], h[3 * i + 1], h[3 * i + 1] ? (double)h[3 * i + 2] / h[3 * i + 1] : 0.0,
-                    h[3 * i + 1] ? (double)h[3 * i] / h[3 * i + 1] : 0.0);
-    }
-#endif
-    if (overflow) {
-        e = hipFreeAsync(overflow, s);
-        if (e != hipSuccess) return hip_fail(e, "hipFreeAsync(path stack overflow)");
-    }
     return LRT_OK;
 }
 
@@ -1370,12 +1313,14 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     const bool lds = !(d->flags & LRT_F_SCENE_GLOBAL) &&
                      sizeof(float4) * (kTraceLdsLevels * kBlock + 4 * (size_t)a.count + a.nlights / 4 + 1) <= 64 * 1024;
     // Kernel policy (measured): v0 -- frames split over lanes, persistent single-wave
-    // blocks on spread tile queues, 4 waves/SIMD -- is fastest on every BASELINE config
-    // (config 2: 0.46 vs 0.64 ms, config 3: 4.15 vs 4.32 ms, config 4: 538 vs 575 ms
-    // for v2s); v1/v2/v2s stay selectable for A/B.
+    // blocks on spread tile queues, 4 waves/SIMD -- is fastest on every BASELINE config.
+    // v3 (regeneration) and v4 (wavefront) stay selectable for A/B; the round-1 per-lane
+    // state machines (v1/v2/v2s, always slower) were removed and their flags are rejected.
     a.regenMin = 0;
     a.lerp = g_ctx.d_lerp;
-    int kflags = d->flags & (LRT_F_SIMPLE | LRT_F_V1 | LRT_F_V2S | LRT_F_V2 | LRT_F_V3 | LRT_F_WAVEFRONT);
+    if (d->flags & (LRT_F_V1 | LRT_F_V2S | LRT_F_V2))
+        return fail(LRT_E_INVALID, "LRT_F_V1/LRT_F_V2S/LRT_F_V2 kernels were removed (use LRT_F_SIMPLE, the default)");
+    int kflags = d->flags & (LRT_F_SIMPLE | LRT_F_V3 | LRT_F_WAVEFRONT);
     if (kflags == 0) kflags = LRT_F_SIMPLE;
     if (want_feat && !(kflags & LRT_F_SIMPLE))
         return fail(LRT_E_INVALID, "features are implemented by the v0 kernel only");
@@ -1385,53 +1330,6 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     if (kflags & LRT_F_V3) {
         if (d->max_depth <= 8) return launch_regen_split<8>(a, lds, d->x_count, d->row_count, d->frames, s);
         return launch_regen_split<64>(a, lds, d->x_count, d->row_count, d->frames, s);
-    }
-    if (!(kflags & LRT_F_SIMPLE)) {
-        PathArgs p;
-        p.cam = a.cam;
-        p.sph = a.sph;
-        p.mats = a.mats;
-        p.lights = a.lights;
-        p.count = a.count;
-        p.nlights = a.nlights;
-        p.width = a.width;
-        p.height = a.height;
-        p.x0 = a.x0;
-        p.xc = a.xc;
-        p.y0 = a.y0;
-        p.rows = a.rows;
-        p.rb = a.rb;
-        p.rp = a.rp;
-        p.rph = a.rph;
-        p.frame0 = a.frame0;
-        p.frames = a.frames;
-        p.maxDepth = a.maxDepth;
-        p.nitems = a.xc * a.rows;
-        p.out = a.out;
-        p.rays = a.rays;
-        p.bv = a.bv;
-        if (kflags & LRT_F_V1) p.bv.on = 0;   // v1 (A/B only) scans linearly
-        p.bvh_stack_offset = 0;
-        // the whole scene (spheres, materials, lights) is staged in LDS when it fits
-        // next to the stack with room for 2 blocks per CU; otherwise it is read from global
-        const bool lds_scene = !(d->flags & LRT_F_SCENE_GLOBAL) &&
-                               2 * paths_lds_bytes(kLdsLevels, true, a.count, a.nlights) <= 160 * 1024;
-        const bool ovf = p.maxDepth > kLdsLevels;
-        // v2 variants: scene in LDS or global x overflow stack x static pixels x BVH
-        const bool stat = (kflags & LRT_F_V2S) != 0;
-        const bool bvh = p.bv.on != 0;
-        auto go = [&](auto lds, auto ovf) -> int {
-            constexpr bool L = decltype(lds)::value, O = decltype(ovf)::value;
-            if (stat) return bvh ? launch_paths<L, true, O, 1, true>(p, s) : launch_paths<L, true, O, 1, false>(p, s);
-            return bvh ? launch_paths<L, true, O, 0, true>(p, s) : launch_paths<L, true, O, 0, false>(p, s);
-        };
-        using T = std::true_type;
-        using F = std::false_type;
-        if (!(kflags & LRT_F_V1)) {
-            if (lds_scene) return ovf ? go(T{}, T{}) : go(T{}, F{});
-            return ovf ? go(F{}, T{}) : go(F{}, F{});
-        }
-        return lds_scene ? launch_paths<true, false, true>(p, s) : launch_paths<false, false, true>(p, s);   // v1
     }
     if (d->max_depth <= 8) return launch_split<8>(a, lds, d->x_count, d->row_count, d->frames, want_feat, s);
     // depth 9..64: one instance (MAXD only decides whether stack levels beyond the 8 in LDS
@@ -1567,6 +1465,7 @@ extern "C" {
 
 const char* lrt_last_error(void) { return t_err.c_str(); }
 const char* lrt_version(void) { return LRT_VERSION_STRING; }
+const char* lrt_last_launch(void) { return g_last_launch; }
 
 int lrt_initialize(void) {
     std::lock_guard<std::mutex> lk(g_mu);
@@ -1576,7 +1475,6 @@ int lrt_initialize(void) {
     g_ctx.device = dev;
     LRT_HIP(hipStreamCreateWithFlags(&g_ctx.stream, hipStreamNonBlocking));
     LRT_HIP(hipMalloc(&g_ctx.d_rays, sizeof(unsigned long long)));
-    LRT_HIP(hipMalloc(&g_ctx.d_queue, sizeof(unsigned int) * kQueueSlots));
     LRT_HIP(hipMalloc(&g_ctx.d_tiles, sizeof(unsigned long long) * kQueueSlots * kTileSetU64));
     LRT_HIP(hipMemset(g_ctx.d_tiles, 0, sizeof(unsigned long long) * kQueueSlots * kTileSetU64));
     {   // parallel.cpp:262's lerpFac per frame number, divided once here instead of per wave
@@ -1607,7 +1505,6 @@ int lrt_shutdown(void) {
     free_scene(g_ctx);
     if (g_ctx.d_frame) (void)hipFree(g_ctx.d_frame);
     if (g_ctx.d_rays) (void)hipFree(g_ctx.d_rays);
-    if (g_ctx.d_queue) (void)hipFree(g_ctx.d_queue);
     if (g_ctx.d_tiles) (void)hipFree(g_ctx.d_tiles);
     g_ctx.d_tiles = nullptr;
     if (g_ctx.d_lerp) (void)hipFree(g_ctx.d_lerp);

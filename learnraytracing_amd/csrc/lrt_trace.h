@@ -99,6 +99,7 @@ LRT_DEV void renorm_lut_fill(float* lut, int tid, int block) {
         lut[j] = rcp_rn(sqrt_rn(d));
     }
 }
+constexpr int kPowTableBytes = 16 * 8 + 16 * 8 + 32 * 8;   // powf tables (lrt_libm.h) staged in LDS
 LRT_DEV F3 normalize_member(F3 v) { float l = length(v); return f3(v.x / l, v.y / l, v.z / l); } // maths.h:19
 LRT_DEV F3 reflect(F3 v, F3 n) { return v + 2.0f * (-dot(v, n) * n); }             // maths.h:100-103
 LRT_DEV bool refract(F3 v, F3 n, float nint, F3& out) {                             // maths.h:106-118
@@ -335,6 +336,22 @@ LRT_DEV int ClosestHitSV(const Ray& r, float tMin, float tMax, const SceneView& 
     tOut = closestT;
     return id;
 }
+// The plain scan over a sphere array (host diagnostics: lrt_bvh_stats checks the BVH
+// against it). Same per-sphere arithmetic and strict-< replacement as HitWorld.
+LRT_DEV int ClosestHit(const F3& o, const F3& d, const float4* sph, int count, float& tOut) {
+    float closestT = kMaxT;
+    int id = -1;
+    for (int i = 0; i < count; ++i) {
+        const float4 s = sph[i];
+        const F3 rs = f3(s.x, s.y, s.z) - o;
+        const float rsProj = dot(rs, d);
+        const float ifHit = dot(rs, rs) - rsProj * rsProj - s.w;
+        SphereRoots(rsProj, ifHit, kMinT, closestT, id, i);
+    }
+    tOut = closestT;
+    return id;
+}
+
 template <bool kBvh = false, int kNS = 0>
 LRT_DEV bool HitWorld(const Ray& r, float tMin, float tMax, const SceneView& sc, Hit& outHit, int& outID) {
     float closestT;

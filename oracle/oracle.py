@@ -19,6 +19,8 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 ORC_PATH = os.path.join(HERE, "liblrt_oracle.so")
 REF_PATH = os.path.join(HERE, "_ref", "libref.so")
+# the reference compiled with random_scene(1000, 1) as its static scene (make ref1000)
+REF1000_PATH = os.path.join(HERE, "_ref", "libref1000.so")
 
 _P = ctypes.c_void_p
 _ll = ctypes.c_longlong
@@ -33,7 +35,6 @@ def build_orc() -> None:
 
 
 _orc = None
-_ref = None
 
 
 def orc():
@@ -61,14 +62,18 @@ def orc():
     return _orc
 
 
-def have_ref() -> bool:
-    return os.path.exists(REF_PATH)
+def have_ref(n: int = 9) -> bool:
+    return os.path.exists(REF_PATH if n == 9 else REF1000_PATH)
 
 
-def ref():
-    global _ref
-    if _ref is None:
-        lib = ctypes.CDLL(REF_PATH)
+_refs = {}
+
+
+def ref(n: int = 9):
+    """The reference's own sources compiled in place: n = 9 its default scene (libref.so),
+    n = 1000 its static scene replaced by random_scene(1000, 1) (libref1000.so)."""
+    if n not in _refs:
+        lib = ctypes.CDLL(REF_PATH if n == 9 else REF1000_PATH)
         for f in ("ref_render_mode_r", "ref_render_mode_p", "ref_render_mode_p_procs"):
             getattr(lib, f).restype = _ll
         lib.ref_render_mode_r.argtypes = [ctypes.c_int] * 5 + [_P]
@@ -83,8 +88,18 @@ def ref():
         lib.ref_hit_world.argtypes = [_P, _P, ctypes.c_float, ctypes.c_float, _P]
         lib.ref_trace.argtypes = [_P, _P, ctypes.c_int, ctypes.c_uint32, _P]
         lib.ref_draw_test.argtypes = [ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]
-        _ref = lib
-    return _ref
+        _refs[n] = lib
+    return _refs[n]
+
+
+def ref_scene(n: int = 9):
+    """The static scene a reference build holds, in the oracle layout (spheres, mats)."""
+    r = ref(n)
+    cnt = r.ref_scene_count()
+    s = np.zeros(4 * cnt, np.float32)
+    m = np.zeros(9 * cnt, np.float32)
+    r.ref_get_scene(_ptr(s), _ptr(m))
+    return s, m
 
 
 # ---- convenience wrappers ---------------------------------------------------------------
@@ -177,10 +192,11 @@ def orc_camera(width, height):
 
 
 def ref_render_p(width, height, frames=1, depth=8, frame0=0, x0=0, xc=None, y0=0, yc=None,
-                 scene=None, cam22=None, procs=1):
-    """Mode P / F through the reference itself. scene=(spheres[36], mats[81]) overrides
-    the reference's 9 statics for the call. Returns (buf, rays)."""
-    r = ref()
+                 scene=None, cam22=None, procs=1, n=9):
+    """Mode P / F through the reference itself. scene=(spheres, mats) overrides the
+    reference's statics for the call; n picks the build (9: libref.so, 1000: libref1000.so).
+    Returns (buf, rays)."""
+    r = ref(n)
     xc = width - x0 if xc is None else xc
     yc = height - y0 if yc is None else yc
     buf = np.zeros((yc, xc, 4), np.float32)

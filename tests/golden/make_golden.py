@@ -1,13 +1,14 @@
 """Generate the golden fixtures in tests/golden/ from the reference ITSELF.
 
-Run in the build container (needs oracle/_ref/libref.so, i.e. /root/reference):
-    make -C oracle ref && python tests/golden/make_golden.py
+Run in the build container (needs /root/reference):
+    make -C oracle ref ref1000 && python tests/golden/make_golden.py
 
-Every fixture except `scene1000_*` comes from the reference's own maths.cpp /
-parallel.cpp compiled in place (oracle/ref_harness.cpp). The 1000-sphere crops come
-from the C restatement (oracle/lrt_oracle.c) because the reference's scene is a fixed
-9-element static; the restatement is pinned to the reference by every other fixture
-(including the 9-sphere fuzz scenes, which exercise the same code with other data).
+Every fixture comes from the reference's own maths.cpp / parallel.cpp compiled in place
+(oracle/ref_harness.cpp). The reference's scene is a fixed static array whose size is
+kSphereCount (parallel.cpp:15-27), so the 1000-sphere crops come from a second build of
+the same sources in which only the two scene initialisers of a scratch copy of
+parallel.cpp (in /tmp, never committed) hold random_scene(1000, 1)
+(oracle/gen_ref_scene.py, `make -C oracle ref1000`).
 Images are stored as float32 RGB (the reference never touches alpha).
 """
 from __future__ import annotations
@@ -170,18 +171,26 @@ def main():
                      "rays": int(rays), "md5_rgba": md5(buf)})
     manifest["fuzz"] = fuzz
 
-    # ---- 1000-sphere crops (restatement; see module docstring) ----------------------------
+    # ---- 1000-sphere crops: the reference itself with random_scene(1000, 1) as its static
+    # scene (oracle/_ref/libref1000.so, `make -C oracle ref1000`; see module docstring).
+    # Small frame counts plus the real spp of configs 4 (64) and 5 (256) on small windows.
     from learnraytracing_amd.scene import random_scene, scene_arrays
-    sph, mat = random_scene(1000, 1)
-    s, m = (np.array(v, np.float32) for v in scene_arrays(sph, mat))
-    for name, (w, h, x0, y0, frames, depth) in {"scene1000_c4_crop": (3840, 2160, 1900, 1000, 2, 8),
-                                                "scene1000_c5_crop": (7680, 4320, 3600, 1900, 1, 8)}.items():
-        buf, rays = oracle.orc_render(w, h, frames, depth, 0, x0, 32, y0, 16, spheres=s, mats=m)
+    assert oracle.have_ref(1000), "build oracle/_ref/libref1000.so first (make -C oracle ref1000)"
+    s, m = (np.array(v, np.float32) for v in scene_arrays(*random_scene(1000, 1)))
+    rs, rm = oracle.ref_scene(1000)
+    assert np.array_equal(rs.view(np.uint32), s.view(np.uint32)) and np.array_equal(rm.view(np.uint32), m.view(np.uint32))
+    for name, (w, h, x0, xc, y0, yc, frames, depth) in {
+            "scene1000_c4_crop": (3840, 2160, 1900, 32, 1000, 16, 2, 8),
+            "scene1000_c5_crop": (7680, 4320, 3600, 32, 1900, 16, 1, 8),
+            "scene1000_c4_s64": (3840, 2160, 1700, 24, 1180, 12, 64, 8),
+            "scene1000_c5_s256": (7680, 4320, 3500, 12, 2300, 8, 256, 8)}.items():
+        buf, rays = oracle.ref_render_p(w, h, frames, depth, 0, x0, xc, y0, yc, procs=8, n=1000)
         arrays[name] = buf[..., :3].copy()
         manifest["fixtures"][name] = {"mode": "P", "scene": "random_scene(1000, seed=1)", "w": w, "h": h,
-                                      "x0": x0, "xc": 32, "y0": y0, "yc": 16, "frame0": 0, "frames": frames,
+                                      "x0": x0, "xc": xc, "y0": y0, "yc": yc, "frame0": 0, "frames": frames,
                                       "max_depth": depth, "rays": int(rays), "md5_rgba": md5(buf),
-                                      "source": "oracle/lrt_oracle.c (restatement)"}
+                                      "source": "reference src/cpu compiled in place with its static scene "
+                                                "replaced by random_scene(1000, 1) (oracle/_ref/libref1000.so)"}
 
     # ---- libm: digests of glibc's sinf/cosf over the path's whole input domain ----------
     k = np.arange(1 << 24, dtype=np.uint32)

@@ -1,0 +1,108 @@
+"""GPU parity for the exact kernel instances behind BASELINE configs 4 and 5.
+
+Configs 4 (3840x2160, 64 spp) and 5 (7680x4320, 256 spp, 8 GPUs) render the 1000-sphere
+scene through the BVH with a pixel's frames spread over 16 lanes (trace_kernel<8, *, true,
+16>) and many lerp rounds per task. Each test renders a window of that geometry at the
+config's REAL spp and checks it bit for bit against the reference's own sources built
+with random_scene(1000, 1) as their static scene (tests/golden: scene1000_c4_s64,
+scene1000_c5_s256), against the C restatement on larger windows, and against the GPU's
+own linear scan (LRT_F_NO_BVH, the reference's HitWorld loop, parallel.cpp:54-73).
+lrt_last_launch() names the instance each render launched, so the tests assert they ran
+the one the benchmark runs. References: parallel.cpp:54-73 (HitWorld), :262,280-286
+(lerp chain over frames).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from learnraytracing_amd import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+NO_BVH = 32
+
+
+def _bitwise(got, want, what):
+    g = got[..., :3]
+    if not np.array_equal(g.view(np.uint32), np.ascontiguousarray(want[..., :3]).view(np.uint32)):
+        d = np.abs(g.astype(np.float64) - want[..., :3].astype(np.float64))
+        raise AssertionError(f"{what}: {int((g != want[..., :3]).any(axis=-1).sum())} pixels differ, "
+                             f"max |diff| {d.max():.3g}")
+
+
+@pytest.fixture(scope="module")
+def scene1000(gpu):
+    from learnraytracing_amd.scene import scene_arrays
+    sph, mat = gpu.random_scene(1000, 1)
+    gpu.set_scene(sph, mat)
+    s, m = (np.array(v, np.float32) for v in scene_arrays(sph, mat))
+    yield s, m
+    gpu.set_scene(*gpu.default_scene())
+
+
+def _render(gpu, flags=0, **kw):
+    job = gpu.Job(flags=flags, **kw)
+    d = job.desc()
+    buf = np.zeros((d.row_count, d.x_count, 4), np.float32)
+    rays = gpu.render_host(job, buf)
+    return buf, rays, L.last_launch()
+
+
+def _assert_instance(info, split, samp="0"):
+    assert info["kernel"] == "trace_kernel" and info["bvh"] == "1" and info["maxd"] == "8", info
+    assert info["split"] == str(split) and info["samp"] == samp, info
+
+
+@pytest.mark.parametrize("name", ["scene1000_c4_s64", "scene1000_c5_s256"])
+def test_config_instance_vs_reference_golden(gpu, scene1000, manifest, images, name):
+    """64 / 256 spp windows of configs 4 / 5 equal the reference's own render."""
+    fx = manifest["fixtures"][name]
+    assert fx["source"].startswith("reference")
+    buf, rays, info = _render(gpu, width=fx["w"], height=fx["h"], frames=fx["frames"], max_depth=fx["max_depth"],
+                              x0=fx["x0"], x_count=fx["xc"], y0=fx["y0"], row_count=fx["yc"])
+    _assert_instance(info, 16)
+    _bitwise(buf, images[name], name)
+    assert rays == fx["rays"]
+
+
+def test_config4_window_vs_oracle_and_linear_scan(gpu, scene1000):
+    """A 64x24 window of config 4 at 64 spp: BVH == C restatement == GPU linear scan."""
+    s, m = scene1000
+    kw = dict(width=3840, height=2160, frames=64, max_depth=8, x0=1880, x_count=64, y0=1000, row_count=24)
+    a, ra, info = _render(gpu, **kw)
+    _assert_instance(info, 16)
+    want, wr = oracle.orc_render(3840, 2160, 64, 8, 0, 1880, 64, 1000, 24, spheres=s, mats=m, threads=16)
+    _bitwise(a, want, "config4 window vs oracle")
+    assert ra == wr
+    b, rb, info_b = _render(gpu, flags=NO_BVH, **kw)
+    assert info_b["bvh"] == "0" and info_b["split"] == "16"
+    assert rb == ra and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_config4_many_tiles_bvh_equals_linear_scan(gpu, scene1000):
+    """Enough 64-spp tiles that the persistent grid refills from its queues several times
+    (every block runs many tasks): BVH == linear scan, rays included."""
+    kw = dict(width=3840, height=2160, frames=64, max_depth=8, x0=1536, x_count=768, y0=900, row_count=96)
+    a, ra, info = _render(gpu, **kw)
+    _assert_instance(info, 16)
+    assert int(info["tasks"]) > int(info["grid"])
+    b, rb, _ = _render(gpu, flags=NO_BVH, **kw)
+    assert rb == ra and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_config5_shard_of_8_vs_oracle(gpu, scene1000):
+    """Rank 3's row-block-cyclic shard of an 8-GPU config-5 frame (row blocks of 8, 256 spp
+    per pixel -- the strong-scaling shape, BVH without sample mode): two row bands of a
+    24-column window against the restatement."""
+    s, m = scene1000
+    W, H, rb, G, ph, y0 = 7680, 4320, 8, 8, 3, 2048
+    a, ra, info = _render(gpu, width=W, height=H, frames=256, max_depth=8, x0=3800, x_count=24, y0=y0,
+                          row_count=16, row_block=rb, row_period=G, row_phase=ph)
+    _assert_instance(info, 16)
+    rays = 0
+    for band in range(2):   # local rows 8*band.. map to y0 + band*rb*G + ph*rb ..
+        gy = y0 + band * rb * G + ph * rb
+        want, wr = oracle.orc_render(W, H, 256, 8, 0, 3800, 24, gy, rb, spheres=s, mats=m, threads=16)
+        _bitwise(a[band * rb:(band + 1) * rb], want, f"config5 shard band {band}")
+        rays += wr
+    assert ra == rays

@@ -100,6 +100,9 @@ def test_modes_need_v0(gpu):
     from learnraytracing_amd import _lib as L
     buf = np.zeros((36, 64, 4), np.float32)
     with pytest.raises(LrtError):
-        gpu.render_host(_job(gpu, 64, 36, 8, 8, flags=64 | L.F_V2S), buf)
+        gpu.render_host_features(_job(gpu, 64, 36, 2, 8, flags=L.F_V3), buf, {"normal": buf.copy()})
     with pytest.raises(LrtError):
-        gpu.render_host_features(_job(gpu, 64, 36, 2, 8, flags=L.F_V2), buf, {"normal": buf.copy()})
+        gpu.render_host_features(_job(gpu, 64, 36, 2, 8, flags=L.F_WAVEFRONT), buf, {"normal": buf.copy()})
+    for removed in (L.F_V1, L.F_V2S, L.F_V2):   # round-1 kernels, removed: rejected loudly
+        with pytest.raises(LrtError):
+            gpu.render_host(_job(gpu, 64, 36, 2, 8, flags=removed), buf)

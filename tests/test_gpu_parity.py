@@ -41,10 +41,10 @@ def test_golden_mode_p(gpu, manifest, images, name):
     assert rays == fx["rays"]
 
 
-@pytest.mark.parametrize("flags", [0, 1, 2, 3, 4, 5, 8, 9, 16, 17, 128, 129])
+@pytest.mark.parametrize("flags", [0, 1, 2, 3, 128, 129, 256, 257])
 @pytest.mark.parametrize("name", ["p_160x90_s4_d8", "p_96x54_s1_d50"])
 def test_golden_kernel_variants(gpu, manifest, images, flags, name):
-    """Every kernel (v2 default, v1 with LRT_F_V1, v0 with LRT_F_SIMPLE), with
+    """Every kernel (v0 default / LRT_F_SIMPLE, v3 LRT_F_V3, v4 LRT_F_WAVEFRONT), with
     LDS-staged or global scene reads, gives the same bits."""
     fx = manifest["fixtures"][name]
     buf, rays = _render(gpu, fx["w"], fx["h"], fx["frames"], fx["max_depth"], flags=flags)
@@ -294,7 +294,7 @@ def test_deterministic_repeat_full_config2(gpu):
 
 
 @pytest.mark.parametrize("n,seed", [(17, 3), (200, 5), (1000, 1), (4096, 7)])
-@pytest.mark.parametrize("kflags", [2, 8, 16, 128, 256])
+@pytest.mark.parametrize("kflags", [2, 128, 256])
 def test_bvh_equals_linear_scan(gpu, n, seed, kflags):
     """The BVH closest hit returns the reference's scan result bit for bit: same
     pixels and ray counts as LRT_F_NO_BVH, for every kernel."""
@@ -354,7 +354,9 @@ def test_cu_reserved_render_stream(gpu):
     from learnraytracing_amd.renderer import RenderStream
     want, wr = _render(gpu, 320, 180, 4, 8)
     job = gpu.Job(width=320, height=180, frame0=0, frames=4, max_depth=8)
-    for reserved in (8, 200):
+    # num_cus - 1 leaves ONE CU: fewer resident blocks than v0's 16 tile queues, and every
+    # queue still needs a block of its own
+    for reserved in (8, 200, torch.cuda.get_device_properties(0).multi_processor_count - 1):
         rs = RenderStream(reserved)
         try:
             buf = torch.zeros((180, 320, 4), dtype=torch.float32, device="cuda")

@@ -36,3 +36,16 @@ def test_config2_full_frame():
     a, ra = oracle.ref_render_p(1280, 720, 4, 8, procs=8)
     b, rb = oracle.orc_render(1280, 720, 4, 8)
     assert ra == rb == 11669343 and np.array_equal(a, b)
+
+
+@pytest.mark.skipif(not oracle.have_ref(1000), reason="oracle/_ref/libref1000.so not built")
+def test_scene1000_window_live():
+    """The reference's 1000-sphere build and the restatement on a fresh window (frames
+    5..20, a row band crossing the horizon): same bits, same rays."""
+    from learnraytracing_amd.scene import random_scene, scene_arrays
+    s, m = (np.array(v, np.float32) for v in scene_arrays(*random_scene(1000, 1)))
+    rs, rm = oracle.ref_scene(1000)
+    assert np.array_equal(rs, s) and np.array_equal(rm, m)
+    a, ra = oracle.ref_render_p(3840, 2160, 16, 8, 5, 1400, 40, 1050, 6, procs=8, n=1000)
+    b, rb = oracle.orc_render(3840, 2160, 16, 8, 5, 1400, 40, 1050, 6, spheres=s, mats=m)
+    assert ra == rb and np.array_equal(a.view(np.uint32), b.view(np.uint32))

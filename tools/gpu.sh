@@ -1,0 +1,63 @@
+#!/bin/bash
+# One parameterised GPU session (replaces round 1's one-off gpu_*.sh scripts).
+#
+#   TAG=r2_x gpurun -- bash tools/gpu.sh STEP [STEP ...]
+#
+# Steps (each under its own timeout; the session stops at the first failure):
+#   test[=K]          pytest -m gpu (optionally -k K)
+#   smoke             __graft_entry__.smoke()
+#   bench=C[,ARGS]    bench.py --config C (ARGS: extra bench flags, ';'-separated)
+#   trace=C[,ARGS]    rocprofv3 --kernel-trace --stats of bench.py --config C --streams 1
+#   pmc=C,GROUP       one rocprofv3 --pmc pass (GROUP: fetch | write | sq | sq2) of bench --config C
+#   py=SCRIPT[,ARGS]  python SCRIPT ARGS (diagnostics under tools/)
+# Output: gpurun_out/$TAG/<step>.log (+ rocprof CSVs).
+cd "$GRAFT_REPO_ROOT" || exit 1
+TAG=${TAG:-latest}
+out=gpurun_out/$TAG
+mkdir -p "$out"
+export TMPDIR=/tmp
+BSTEPS=${BSTEPS:-20}
+declare -A PMC=(
+  [fetch]="FETCH_SIZE"
+  [write]="WRITE_SIZE"
+  [sq]="SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_ANY"
+  [sq2]="SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM"
+)
+run() {   # run NAME SECONDS CMD...
+  local name=$1 t=$2
+  shift 2
+  local t0=$SECONDS
+  timeout -k 10 "$t" "$@" > "$out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc ($((SECONDS - t0)) s)"
+  tail -n "${TAILN:-3}" "$out/$name.log" | cut -c1-400
+  if [ $rc -ne 0 ]; then echo "stopping after $name"; exit $rc; fi
+}
+i=0
+for s in "$@"; do
+  i=$((i + 1))
+  key=${s%%=*}
+  val=${s#*=}
+  [ "$val" = "$s" ] && val=""
+  c=${val%%,*}
+  rest=""
+  [[ "$val" == *,* ]] && rest=${val#*,}
+  extra=${rest//;/ }
+  case $key in
+    test)
+      if [ -n "$val" ]; then
+        run "test$i" 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "$val"
+      else
+        run "test$i" 1100 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread
+      fi ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) TAILN=1 run "bench_c${c}_$i" 600 python bench.py --config "$c" --steps "$BSTEPS" $extra ;;
+    trace) run "trace_c${c}_$i" 600 rocprofv3 --kernel-trace --stats -d "$out" -o "trace_c${c}" --output-format csv -- \
+             python3 bench.py --config "$c" --steps "$BSTEPS" --streams 1 --no-cpu-baseline $extra ;;
+    pmc)   g=${rest%%,*}
+           run "pmc_c${c}_$g" 300 rocprofv3 --pmc ${PMC[$g]} -d "$out" -o "pmc_c${c}_$g" --output-format csv -- \
+             python3 bench.py --config "$c" --steps 2 --warmup 1 --streams 1 --no-cpu-baseline --no-extra-legs ;;
+    py)    run "py$i" 600 python ${val//,/ } ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
