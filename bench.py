@@ -1,23 +1,32 @@
 #!/usr/bin/env python3
 """bench.py — throughput of the MI355X path tracer on BASELINE.json's headline metric.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5] [--scaling strong|weak]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 A step is one pass of the hot path over one batch: every rank renders its
-row-block-cyclic share of the config's image for all of that step's samples (one
-kernel launch), and for N > 1 the shards are gathered to rank 0 over RCCL and
-assembled there (the gather of step k overlaps the render of step k+1; the timed
-region ends after the last gather and assembly).
+row-block-cyclic share of the config's W x H image at the config's spp (one kernel
+launch), and for N > 1 the shards are gathered to rank 0 over RCCL and assembled there
+(the gather of step k overlaps the render of step k+1; the timed region ends after the
+last gather and assembly).
 
-Scaling is WEAK by default: per-GPU work is fixed at the config's frame
-(W x H x spp pixel-samples); with N GPUs the frame gets N x spp samples per pixel
-(each GPU renders 1/N of the rows at N x spp). --scaling strong keeps spp fixed.
+Scaling is STRONG by default: the frame (W x H x spp) is fixed and split over the N
+GPUs, so config 2 at N = 8 is still 1280x720 at 4 spp (each GPU renders 1/8 of the
+rows) and config 5 is 7680x4320 at 256 spp in total. --scaling weak keeps the per-GPU
+work fixed instead (N x spp samples per pixel).
 
 `value` = counted rays of all ranks / max-over-ranks wall time of the K steps, in
 Mray/s, the reference's own formula (src/cpu/main.cpp:188-189; rays counted as
 parallel.cpp:122,204). Inputs are resident in HBM (the scene is uploaded once); no
 host transfer is inside the timed region.
+
+Besides the timed region (unless --no-extra-legs):
+  * `ms_per_launch_alone`: the same launches one at a time on one stream, each bracketed
+    by HIP events on that stream -- the duration the roofline objects divide by;
+  * `end_to_end`: render (+ gather and assembly) + the D2H copy of the frame into pinned
+    host memory on rank 0, pipelined over two slots;
+  * `cpu_baseline` (all host cores) and `cpu_baseline_1core`: the reference's own
+    TraceRowJob body (oracle/_ref, rank 0 at N = 1 only, before the GPU is touched).
 
 Rank 0 prints ONE JSON line on stdout; progress goes to stderr.
 """
@@ -41,41 +50,64 @@ CONFIGS = {
 }
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md, chip-level parameters (spec)
 BYTES_PER_PIXEL_SAMPLE = 24.0    # 12 B read + 12 B write of RGB per pixel-sample
+# VALU: 256 CUs x 4 SIMD32 x 32 lanes per clock x 2.4 GHz = 78.6 T lane-operations/s
+# (the 157.3 TFLOP/s FP32 vector peak of MI355X_MICROARCH.md counts an FMA as 2)
+VALU_LANE_PEAK_T = 256 * 4 * 32 * 2.4e9 / 1e12
+VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2   # wave64 VALU instructions/s (2 cycles each per SIMD)
+PMC_INDEX = os.path.join(ROOT, "profiles", "pmc_index.json")
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(cfg, budget_s: float):
-    """Time the reference's own TraceRowJob body (oracle/_ref, forked worker processes,
-    per-pixel seeds) -- or the C restatement if _ref is absent -- on this host."""
+def workload(config: int, world: int = 1, scaling: str = "strong", spp=None, depth=None, shard_of: int = 1):
+    """The per-rank render of `config` at N = world: shards = row shards of the frame,
+    spp_total = samples per pixel of the whole frame (each rank renders its rows at that
+    spp). Pure function (tested on CPU)."""
+    if scaling not in ("strong", "weak"):
+        raise ValueError("scaling must be strong or weak")
+    cfg = dict(CONFIGS[config])
+    if spp:
+        cfg["spp"] = spp
+    if depth is not None:
+        cfg["depth"] = depth
+    shards = world if world > 1 else max(1, shard_of)
+    cfg["shards"] = shards
+    cfg["spp_total"] = cfg["spp"] * shards if scaling == "weak" else cfg["spp"]
+    cfg["pixel_samples_total"] = cfg["width"] * cfg["height"] * cfg["spp_total"]
+    return cfg
+
+
+def cpu_baseline(cfg, budget_s: float, cores: int):
+    """Time the reference's own TraceRowJob body (oracle/_ref: libref.so, or libref1000.so
+    whose static scene is random_scene(1000, 1)) in forked worker processes with per-pixel
+    seeds -- or the C restatement if _ref is absent -- on this host, for about budget_s."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
     import oracle  # test infrastructure: the baseline leg only
 
-    cores = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
-    cores = max(1, min(cores, os.cpu_count() or 1))
     w, h, depth = cfg["width"], cfg["height"], cfg["depth"]
-    if cfg["scene"] == "default":
+    n = 9 if cfg["scene"] == "default" else 1000
+    if n == 9:
         x0, xc, y0, yc = 0, w, 0, h
         spheres = mats = None
         what = f"full {w}x{h} frames"
     else:
         from learnraytracing_amd.scene import random_scene, scene_arrays
-        import numpy as np
         s, m = scene_arrays(*random_scene(1000, 1))
         spheres, mats = np.array(s, np.float32), np.array(m, np.float32)
         xc, yc = 128, 32
         x0, y0 = (w - xc) // 2, (h - yc) // 2
         what = f"{xc}x{yc} centre crop of {w}x{h}"
-    use_ref = oracle.have_ref() and spheres is None
+    use_ref = oracle.have_ref(n)
     kind = "reference" if use_ref else "port"
     rays = 0
     frames = 0
     t0 = time.perf_counter()
     while True:
         if use_ref:
-            _, r = oracle.ref_render_p(w, h, 1, depth, frames, x0, xc, y0, yc, procs=cores)
+            _, r = oracle.ref_render_p(w, h, 1, depth, frames, x0, xc, y0, yc, procs=cores, n=n)
         else:
             _, r = oracle.orc_render(w, h, 1, depth, frames, x0, xc, y0, yc, spheres=spheres, mats=mats,
                                      threads=cores)
@@ -86,47 +118,25 @@ def cpu_baseline(cfg, budget_s: float):
         dt = time.perf_counter() - t0
         if dt >= budget_s:
             break
-    src = "oracle/_ref (reference maths.cpp+parallel.cpp, clang -O2)" if use_ref else "oracle/lrt_oracle.c"
-    return {"value": rays / dt / 1e6, "unit": "Mray/s", "cores": cores, "kind": kind,
+    src = (f"oracle/_ref/{'libref.so' if n == 9 else 'libref1000.so'} (reference maths.cpp+parallel.cpp, clang -O2)"
+           if use_ref else "oracle/lrt_oracle.c")
+    return {"value": round(rays / dt / 1e6, 3), "unit": "Mray/s", "cores": cores, "kind": kind,
             "sample": f"{what}, {frames} frame(s) x 1 spp, {depth} bounces, per-pixel seeds, "
                       f"{rays} rays in {dt:.2f} s, {cores} {'processes' if use_ref else 'threads'}; {src}"}
 
 
-def kernel_name(kernel: str, frames: int) -> str:
-    if kernel == "auto":   # mirrors render_device's policy in lrt_hip.hip
-        kernel = "v0"
-    return {"v0": "trace_kernel", "v1": "paths_kernel", "v3": "regen_kernel", "wf": "wf_extend"}.get(kernel, "paths2_kernel")
-
-
-def read_traffic(cfg_name: str):
-    """HBM bytes per launch of trace_kernel from the committed PMC run, if any."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def read_pmc(key: str):
+    """Per-launch counters of trace_kernel for `key` (e.g. "config2_n1") from the committed
+    rocprofv3 passes (profiles/pmc_index.json -> profiles/<run>/summary_<config>.json)."""
     try:
+        with open(PMC_INDEX) as f:
+            src = json.load(f)[key]
+        p = os.path.join(ROOT, "profiles", src)
         with open(p) as f:
-            d = json.load(f)
-        e = d.get(cfg_name)
-        return (e["bytes_per_launch"], os.path.relpath(p, ROOT)) if e else (None, None)
-    except (OSError, ValueError, KeyError):
-        return None, None
-
-
-def read_valu(cfg_name: str):
-    """VALU issue fraction and lane utilisation of trace_kernel from the summary of the
-    committed PMC run that pmc_traffic.json points at (the path's real bound)."""
-    try:
-        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
-            src = json.load(f)[cfg_name]["source"]
-        sp = os.path.join(ROOT, "profiles", src, "summary.json")
-        with open(sp) as f:
             s = json.load(f)
-        c = s["counters_per_launch"]
-        return {"issue_frac": round(s["valu_issue_frac_of_peak"], 4),
-                "valu_insts_per_launch": c["SQ_INSTS_VALU"],
-                "lane_util": round(c["SQ_THREAD_CYCLES_VALU"] / (c["SQ_ACTIVE_INST_VALU"] * 64), 4),
-                "note": "wave64 VALU instructions issued / (1024 SIMDs x 1 per 2 cycles at 2.4 GHz); "
-                        "lane_util = active lanes per VALU instruction / 64",
-                "source": os.path.relpath(sp, ROOT)}
-    except (OSError, ValueError, KeyError, ZeroDivisionError):
+        s["path"] = os.path.relpath(p, ROOT)
+        return s
+    except (OSError, ValueError, KeyError):
         return None
 
 
@@ -136,25 +146,25 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
     ap.add_argument("--row-block", type=int, default=8)
     ap.add_argument("--streams", type=int, default=2,
                     help="render streams the steps rotate over: step k+1 starts in the CU slots step k's "
                          "persistent grid frees during its tail (each step writes its own buffer)")
-    ap.add_argument("--spp", type=int, default=None, help="diagnostic: override the config's spp per GPU")
+    ap.add_argument("--spp", type=int, default=None, help="diagnostic: override the config's spp")
     ap.add_argument("--depth", type=int, default=None, help="diagnostic: override the config's bounce budget")
     ap.add_argument("--shard-of", type=int, default=1,
-                    help="diagnostic (1 process): render only rank 0's shard of an N-GPU weak-scaling run, "
-                         "no gather -- the per-GPU render time at N GPUs, measured on one")
+                    help="diagnostic (1 process): render only rank 0's shard of an N-GPU run, no gather -- "
+                         "the per-GPU render at N GPUs, measured on one")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=None, help="seconds of CPU-baseline timing")
+    ap.add_argument("--no-extra-legs", action="store_true",
+                    help="only the timed region (profiling runs): no launch-alone, end-to-end or CPU legs")
+    ap.add_argument("--cpu-budget", type=float, default=None, help="seconds of all-core CPU-baseline timing")
     ap.add_argument("--scene-global", action="store_true", help="read spheres from global memory, not LDS")
     ap.add_argument("--reserve-cus", type=int, default=None,
                     help="CUs the render stream leaves free for other streams (default 0)")
-    ap.add_argument("--kernel", choices=["auto", "v0", "v1", "v2", "v2s", "v3", "wf"], default="auto",
-                    help="auto: the library's policy (default); v0: one pixel per lane (LRT_F_SIMPLE); "
-                         "v1: unscheduled state machine; v2: phase-scheduled persistent; v2s[N]: "
-                         "phase-scheduled, N static pixels per lane")
+    ap.add_argument("--kernel", choices=["auto", "v0", "v3", "wf"], default="auto",
+                    help="auto: the library's policy (v0); v3: path regeneration; wf: wavefront (A/B)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -162,21 +172,20 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: WORLD_SIZE={world} but --gpus {args.gpus}; using WORLD_SIZE")
-    cfg = dict(CONFIGS[args.config])
-    if args.spp:
-        cfg["spp"] = args.spp
-    if args.depth is not None:
-        cfg["depth"] = args.depth
+    cfg = workload(args.config, world, args.scaling, args.spp, args.depth, args.shard_of)
     cfg_name = f"config{args.config}"
+    extra = not args.no_extra_legs
 
-    # CPU baseline first: rank 0 at N=1 only, before anything touches the GPU.
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    # CPU baselines first: rank 0 at N=1 only, before anything touches the GPU.
+    cpu = cpu1 = None
+    if rank == 0 and world == 1 and extra and not args.no_cpu_baseline:
         cores = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
-        budget = args.cpu_budget if args.cpu_budget is not None else max(1.5, 15.0 / max(1, cores))
-        log(f"cpu baseline ({budget:.1f} s budget) ...")
-        cpu = cpu_baseline(cfg, budget)
-        log(f"cpu baseline: {cpu['value']:.1f} Mray/s ({cpu['kind']}, {cpu['cores']} cores)")
+        cores = max(1, min(cores, os.cpu_count() or 1))
+        budget = args.cpu_budget if args.cpu_budget is not None else max(1.5, 15.0 / cores)
+        log(f"cpu baseline ({budget:.1f} s on {cores} cores, then 6 s on 1 core) ...")
+        cpu = cpu_baseline(cfg, budget, cores)
+        cpu1 = cpu_baseline(cfg, 6.0, 1)
+        log(f"cpu baseline: {cpu['value']:.1f} Mray/s ({cpu['kind']}, {cores} cores), 1 core {cpu1['value']:.2f}")
 
     import torch
     import torch.distributed as dist
@@ -191,6 +200,7 @@ def main():
         else:
             dist.init_process_group(backend)
     import learnraytracing_amd as lrt
+    from learnraytracing_amd import _lib as L
     from learnraytracing_amd.dist import gather_to_root, max_shard_rows, shard_rows
     from learnraytracing_amd.renderer import unshard_tensor
 
@@ -208,12 +218,11 @@ def main():
     if cfg["scene"] == "random1000":
         lrt.set_scene(*lrt.random_scene(1000, 1))
     W, H, D = cfg["width"], cfg["height"], cfg["depth"]
-    shards = world if world > 1 else max(1, args.shard_of)   # row shards of the frame
-    spp_total = cfg["spp"] * shards if args.scaling == "weak" else cfg["spp"]
+    shards, spp_total = cfg["shards"], cfg["spp_total"]
     rb = H if shards == 1 else args.row_block
     max_rows = max_shard_rows(H, rb, shards)
     rows = shard_rows(H, rb, shards, rank)
-    flags = (1 if args.scene_global else 0) | {"auto": 0, "v0": 2, "v1": 4, "v2": 16, "v2s": 8, "v3": 128, "wf": 256}[args.kernel]
+    flags = (1 if args.scene_global else 0) | {"auto": 0, "v0": 2, "v3": 128, "wf": 256}[args.kernel]
     job = lrt.Job(width=W, height=H, frame0=0, frames=spp_total, max_depth=D, row_block=rb,
                   row_period=shards, row_phase=rank, row_count=rows, flags=flags)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -223,43 +232,61 @@ def main():
     rays = torch.zeros(1, dtype=torch.int64, device=dev)
     gathered = [torch.empty((world, max_rows, W, 4), dtype=torch.float32, device=dev) if rank == 0 and world > 1
                 else None for _ in range(nslots)]
-    frame = torch.empty((H, W, 4), dtype=torch.float32, device=dev) if rank == 0 and world > 1 else None
+    frames_out = [torch.empty((H, W, 4), dtype=torch.float32, device=dev) if rank == 0 and world > 1 else None
+                  for _ in range(nslots)]
     stream = torch.cuda.current_stream(dev)
-    # render streams (the first is the current stream); frame assembly on its own stream
+    # render streams (the first is the current stream); frame assembly and D2H on their own
     rstreams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(nstreams - 1)]
     astream = torch.cuda.Stream(device=dev) if world > 1 else stream
+    cstream = torch.cuda.Stream(device=dev)
+    host = None   # pinned frame copies (end-to-end leg)
+    pending = []   # (work, slot, k) of steps whose gather / D2H is not yet enqueued
 
-    pending = []   # (work, slot) of gathers not yet assembled
-
-    def assemble(work, slot):
-        with torch.cuda.stream(astream):
-            if work is not None:
-                work.wait()   # the assembly stream waits for the gather
-            if rank == 0:
-                unshard_tensor(gathered[slot], frame, W, H, rb, world, astream)
+    def finish(work, slot, d2h, rdone):
+        """Assemble slot's frame on rank 0 (after its gather), then optionally copy it to
+        pinned host memory; the slot's next render waits for both."""
+        done = None
+        if world > 1:
             done = torch.cuda.Event()
-            done.record(astream)
-        # the slot's next render (and so its next gather) waits until this one was gathered
-        rstreams[slot % nstreams].wait_event(done)
+            with torch.cuda.stream(astream):
+                if work is not None:
+                    work.wait()   # the assembly stream waits for the gather
+                if rank == 0:
+                    unshard_tensor(gathered[slot], frames_out[slot], W, H, rb, world, astream)
+                done.record(astream)
+        if d2h and rank == 0:
+            cstream.wait_event(done if done is not None else rdone)
+            with torch.cuda.stream(cstream):
+                host[slot].copy_(frames_out[slot] if world > 1 else bufs[slot], non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(cstream)
+        if done is not None:
+            rstreams[slot % nstreams].wait_event(done)
 
-    def step(k, events=None):
+    def step(k, d2h=False):
         slot = k % nslots
         rs = rstreams[k % nstreams]
-        if events is not None:
-            events[0].record(rs)
         lrt.render_tensor(job, bufs[slot], rays, rs)
-        if events is not None:
-            events[1].record(rs)
+        rdone = None
+        if d2h and world == 1:
+            rdone = torch.cuda.Event()
+            rdone.record(rs)
+        work = None
         if world > 1:
             with torch.cuda.stream(rs):   # the gather is ordered after this step's render
                 _, work = gather_to_root(bufs[slot], max_rows, world, rank, gathered=gathered[slot], async_op=True)
-            while pending:
-                assemble(*pending.pop(0))
-            pending.append((work, slot))
+        while pending:
+            finish(*pending.pop(0))
+        pending.append((work, slot, d2h, rdone))
 
     def drain():
         while pending:
-            assemble(*pending.pop(0))
+            finish(*pending.pop(0))
+
+    def sync_all():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
 
     log(f"rank {rank}/{world}: {cfg_name} {W}x{H} spp_total={spp_total} depth={D} rows={rows} "
         f"row_block={rb} scaling={args.scaling}")
@@ -269,47 +296,90 @@ def main():
     for k in range(warmup):
         step(k)
     drain()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    sync_all()
     rays.zero_()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    sync_all()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(warmup + k, ev[k])
+        step(warmup + k)
     drain()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
-    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / max(1, args.steps)
+    timed_rays = float(rays.item())
+    launch_info = L.last_launch()
 
-    stats = torch.tensor([elapsed, float(rays.item()), kernel_ms], dtype=torch.float64,
+    # ---- extra legs: each launch alone (roofline duration), end to end (D2H included)
+    alone_ms = e2e_s = None
+    e2e_steps = 0
+    if extra:
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+        scratch = torch.zeros(1, dtype=torch.int64, device=dev)
+        for k in range(args.steps):
+            ev[k][0].record(stream)
+            lrt.render_tensor(job, bufs[0], scratch, stream)
+            ev[k][1].record(stream)
+        torch.cuda.synchronize()
+        alone_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+        if rank == 0:
+            host = [torch.empty((H, W, 4), dtype=torch.float32, pin_memory=True) for _ in range(nslots)]
+        e2e_steps = max(1, min(args.steps, 10))
+        sync_all()
+        t2 = time.perf_counter()
+        for k in range(e2e_steps):
+            step(k, d2h=True)
+        drain()
+        torch.cuda.synchronize()
+        e2e_s = time.perf_counter() - t2
+        if world > 1:
+            dist.barrier()
+
+    stats = torch.tensor([elapsed, timed_rays, alone_ms or 0.0, e2e_s or 0.0], dtype=torch.float64,
                          device=dev if backend == "nccl" else "cpu")
     if world > 1:
-        t = stats[0:1].clone()
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
         r = stats[1:2].clone()
         dist.all_reduce(r, op=dist.ReduceOp.SUM)
-        km = stats[2:3].clone()
-        dist.all_reduce(km, op=dist.ReduceOp.MAX)
-        stats = torch.cat([t, r, km])
-    elapsed, total_rays, kernel_ms = (float(x) for x in stats.tolist())
+        mx = stats.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        stats = torch.cat([mx[0:1], r, mx[2:4]])
+    elapsed, total_rays, alone_ms, e2e_s = (float(x) for x in stats.tolist())
 
     if rank == 0:
         value = total_rays / elapsed / 1e6
+        rays_per_step = total_rays / args.steps
+        ms_step = elapsed / args.steps * 1e3
         pix_samples = rows * W * spp_total                     # one launch on rank 0
         alg_bytes = BYTES_PER_PIXEL_SAMPLE * pix_samples
-        achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-        traffic, traffic_src = read_traffic(f"{cfg_name}_n{world}")
-        valu = read_valu(f"{cfg_name}_n{world}")
-        if valu:   # the committed launch's VALU instructions over this run's wall time per launch
-            valu["issue_frac_effective"] = round(valu["valu_insts_per_launch"] / (elapsed / args.steps)
-                                                 / (256 * 4 * 2.4e9 / 2), 4)
+        key = f"{cfg_name}_n{shards}" if args.scaling == "strong" or shards == 1 else f"{cfg_name}_n{shards}_weak"
+        pmc = read_pmc(key) if not (args.spp or args.depth is not None or args.kernel not in ("auto", "v0")) else None
+        dur_ms = alone_ms if alone_ms else ms_step
+        hbm = {"bound": "hbm", "achieved": round(alg_bytes / (dur_ms * 1e-3) / 1e9, 3), "peak": HBM_PEAK_GBS,
+               "unit": "GB/s", "frac": round(alg_bytes / (dur_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
+               "traffic": pmc["hbm_bytes_per_launch"] if pmc and "hbm_bytes_per_launch" in pmc else None,
+               "algorithmic_bytes_per_launch": alg_bytes,
+               "note": "24 B per pixel-sample (SURVEY 8(d)) x the launch's pixel-samples over one launch's "
+                       "duration alone (ms_per_launch_alone); traffic = corrected 2 x FETCH_SIZE + WRITE_SIZE "
+                       "per launch from the committed PMC pass"}
+        roof = hbm
+        if pmc and "lane_ops_per_launch" in pmc:
+            lane_ops = pmc["lane_ops_per_launch"]
+            achieved_t = lane_ops / (dur_ms * 1e-3) / 1e12
+            roof = {"bound": "valu", "achieved": round(achieved_t, 3), "peak": round(VALU_LANE_PEAK_T, 2),
+                    "unit": "TFLOP/s", "frac": round(achieved_t / VALU_LANE_PEAK_T, 4),
+                    "traffic": hbm["traffic"], "kernel": "trace_kernel",
+                    "lane_ops_per_launch": lane_ops,
+                    "issue_frac": round(pmc["valu_insts_per_launch"] / (dur_ms * 1e-3) / VALU_ISSUE_PEAK, 4),
+                    "lane_util": pmc["lane_util"],
+                    "duration_ms": round(dur_ms, 4),
+                    "source": pmc["path"],
+                    "note": "FP32 VALU lane-operations/s: SQ_INSTS_VALU x 64 x lane_util per launch "
+                            "(lane_util = SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU x 64), committed PMC "
+                            "pass) over one launch's duration alone, measured here with HIP events; peak = "
+                            "256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T lane-ops/s (the 157.3 TFLOP/s "
+                            "FP32 vector peak counts an FMA as 2); frac = issue_frac x lane_util"}
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -317,46 +387,39 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step": round(ms_step, 4),
+            "ms_per_launch_alone": round(alone_ms, 4) if alone_ms else None,
             "higher_is_better": True,
             "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: procedural sphere scene (no dataset), per-pixel seeded XorShift32 streams",
             "config": {
-                "workload": f"{cfg_name}: {W}x{H}, {cfg['spp']} spp per GPU, {D} bounces, "
-                            f"{'reference 9-sphere scene' if cfg['scene'] == 'default' else 'random_scene(1000, seed=1)'}",
-                "width": W, "height": H, "spp_per_gpu": cfg["spp"], "spp_total": spp_total, "max_depth": D,
-                "rays_per_step": int(total_rays / args.steps),
+                "workload": f"{cfg_name}: {W}x{H}, {spp_total} spp"
+                            + (" per pixel over the whole frame" if args.scaling == "strong" else
+                               f" ({cfg['spp']} per GPU, weak scaling)")
+                            + f", {D} bounces, "
+                            + ("reference 9-sphere scene" if cfg["scene"] == "default" else "random_scene(1000, seed=1)"),
+                "width": W, "height": H, "spp_total": spp_total, "max_depth": D,
+                "rays_per_step": int(rays_per_step),
                 "parallelism": f"rows: row-block-cyclic x{world} (block {rb}), RCCL gather to rank 0"
                 if world > 1 else ("single GPU" if shards == 1 else
                                    f"DIAGNOSTIC: rank 0's shard of {shards} (block {rb}), no gather"),
                 "scene_reads": "global" if args.scene_global else "LDS-staged",
-                "reserved_cus": reserve,
                 "render_streams": nstreams,
-                "kernel": args.kernel,
+                "kernel": launch_info.get("kernel", args.kernel),
+                "instance": " ".join(f"{k}={v}" for k, v in launch_info.items() if k != "kernel"),
             },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 3),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 6),
-                "traffic": traffic,
-                "kernel": kernel_name(args.kernel, spp_total),
-                "kernel_ms": round(kernel_ms, 4),
-                "algorithmic_bytes_per_launch": alg_bytes,
-                "effective_ms_per_launch": round(elapsed / args.steps * 1e3, 4),
-                "achieved_effective": round(alg_bytes / (elapsed / args.steps) / 1e9, 3),
-                "note": "24 B per pixel-sample (SURVEY 8(d)); the path is VALU-bound, HBM frac is "
-                        "reported as north_star asks" + (f"; traffic from {traffic_src}" if traffic_src else "")
-                        + (f"; consecutive steps run on {nstreams} streams and their launches overlap "
-                           "(each fills the CU slots the previous one frees in its tail), so kernel_ms "
-                           "includes the overlap; achieved_effective uses the wall time per launch"
-                           if nstreams > 1 else ""),
-            },
-            "valu": valu,
+            "roofline": roof,
+            "roofline_hbm": hbm,
+            "end_to_end": {
+                "value": round(total_rays / args.steps * e2e_steps / e2e_s / 1e6, 3), "unit": "Mray/s",
+                "ms_per_step": round(e2e_s / e2e_steps * 1e3, 4), "steps": e2e_steps,
+                "what": "render" + (" + RCCL gather + assembly" if world > 1 else "")
+                        + " + D2H of the RGBA frame into pinned host memory on rank 0, pipelined over 2 slots",
+            } if e2e_s else None,
             "cpu_baseline": cpu,
+            "cpu_baseline_1core": cpu1,
         }
         print(json.dumps(out), flush=True)
     if rstream is not None:

@@ -41,7 +41,13 @@ def gather_to_root(local, max_rows: int, world: int, rank: int, gathered=None, g
                    async_op: bool = False):
     """Gather every rank's [max_rows, W, 4] shard buffer into rank 0's
     [world, max_rows, W, 4] tensor (`gathered`, allocated if None).
-    Returns (gathered_or_None, work_or_None)."""
+    Returns (gathered_or_None, work_or_None).
+
+    ONE code path for every backend: `dist.gather` of the shard into the rows of
+    `gathered`. RCCL ("nccl") moves the device tensors over xGMI directly; gloo moves host
+    tensors only, so a cuda shard under gloo (rehearsing N > 1 on one GPU) is staged
+    through host copies around the same call -- CPU tensors under gloo (tests) take the
+    exact lines the RCCL run takes."""
     import torch
     import torch.distributed as dist
 
@@ -49,22 +55,18 @@ def gather_to_root(local, max_rows: int, world: int, rank: int, gathered=None, g
         raise ValueError("shard buffers must be padded to max_rows rows")
     if world == 1:
         return local.unsqueeze(0), None
-    if local.is_cuda and dist.get_backend(group) == "gloo":
-        # gloo gathers host tensors only (used to rehearse N>1 on one GPU / on CPU)
-        host = local.cpu()
-        hout = list(torch.empty((world,) + tuple(local.shape), dtype=local.dtype).unbind(0)) if rank == 0 else None
-        dist.gather(host, gather_list=hout, dst=0, group=group)
-        if rank == 0:
-            if gathered is None:
-                gathered = torch.empty((world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
-            gathered.copy_(torch.stack(hout))
-        return gathered, None
+    stage = local.is_cuda and dist.get_backend(group) == "gloo"
+    send = local.cpu() if stage else local
     out: Optional[List] = None
+    recv = None
     if rank == 0:
         if gathered is None:
             gathered = torch.empty((world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
-        out = list(gathered.unbind(0))
+        recv = torch.empty(gathered.shape, dtype=gathered.dtype) if stage else gathered
+        out = list(recv.unbind(0))
     else:
         gathered = None
-    work = dist.gather(local, gather_list=out, dst=0, group=group, async_op=async_op)
+    work = dist.gather(send, gather_list=out, dst=0, group=group, async_op=async_op and not stage)
+    if stage and rank == 0:
+        gathered.copy_(recv)
     return gathered, work
