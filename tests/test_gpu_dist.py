@@ -72,19 +72,25 @@ def test_two_rank_gpu_shards_assemble_bitwise(gpu, tmp_path, world, rb, frames):
     assert int(np.load(tmp_path / "rays.npy")[0]) == want_rays
 
 
-def test_bench_two_ranks_gloo(gpu):
+@pytest.mark.parametrize("scaling", ["strong", "weak"])
+def test_bench_two_ranks_gloo(gpu, scaling):
     """bench.py --gpus 2 over gloo on one GPU: one JSON line from rank 0 with the
-    aggregate of both ranks (weak scaling: 8 spp over the two row shards)."""
+    aggregate of both ranks. Strong scaling (the default) renders config 2's own frame
+    (4 spp over the two row shards: exactly the 1-GPU ray count); weak renders 8 spp."""
     env = dict(os.environ, LRT_DIST_BACKEND="gloo")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "3", "--warmup", "1"]
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--scaling", scaling]
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, out.stdout
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["cpu_baseline"] is None
-    assert d["config"]["spp_total"] == 8
-    assert 2.0e7 < d["config"]["rays_per_step"] < 2.6e7   # ~2 x config 2's 11.67 M rays
+    assert d["n_gpus"] == 2 and d["scaling"] == scaling and d["cpu_baseline"] is None
+    if scaling == "strong":
+        assert d["config"]["spp_total"] == 4
+        assert d["config"]["rays_per_step"] == 11669343   # config 2's frame, any sharding
+    else:
+        assert d["config"]["spp_total"] == 8
+        assert 2.0e7 < d["config"]["rays_per_step"] < 2.6e7   # ~2 x config 2's 11.67 M rays
     assert d["value"] > 0
