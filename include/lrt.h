@@ -242,6 +242,20 @@ int lrt_libm_eval_device(int kind, const float* d_in, float* d_out, long long n)
  * traversal for the scan's winner and for one other sphere per ray. */
 int lrt_bvh_stats(const lrt_sphere* spheres, int count, const float* rays, int n, double* out);
 
+/* Scatter probe (no render): the device Scatter in the reference's shape (lrt_trace.h;
+ * parallel.cpp:78-196 `bool Scatter(mat, r_in, rec, attenuation, scattered, outLightE,
+ * inoutRayCount)`, RNG state explicit) over the given scene, n cases. Case i: material
+ * ids[i] scatters the ray rays[6i..6i+5] (origin, direction; normalised as the Ray ctor
+ * does) at the hit recs[7i..7i+6] (pos, normal, t) from RNG state seeds[i]. Outputs:
+ * out[12i..] = attenuation, scattered origin, scattered direction, outLightE; ret[i] =
+ * Scatter's result (0: absorbed); counted[i] = shadow rays counted; state[i] = the RNG
+ * state after. Scenes above 16 spheres trace shadow rays through the BVH. on_device = 0
+ * runs the host build of the same code, 1 one thread per case on the current device.
+ * Host pointers either way; blocking. */
+int lrt_scatter_eval(const lrt_sphere* spheres, const lrt_material* materials, int count,
+                     const int* ids, const float* rays, const float* recs, const uint32_t* seeds,
+                     int n, float* out, int* ret, int* counted, uint32_t* state, int on_device);
+
 #ifdef __cplusplus
 }
 #endif

@@ -68,8 +68,8 @@ int main(int argc, char** argv) {
     }
     double s = total_s / frames;
     /* main.cpp:188-189 */
-    printf("%.2fms (%.1f FPS) %.1fMrays/s %.2fMrays/frame frames %i\n", s * 1000.0, 1.0 / s,
-           (double)total_rays / frames / s * 1.0e-6, (double)total_rays / frames * 1.0e-6, frames);
+    printf("%.2fms (%.1f FPS) %.1fMrays/s %.2fMrays/frame frames %i rays %lld\n", s * 1000.0, 1.0 / s,
+           (double)total_rays / frames / s * 1.0e-6, (double)total_rays / frames * 1.0e-6, frames, total_rays);
     const size_t plen = ppm ? strlen(ppm) : 0;
     if (ppm && plen > 4 && strcmp(ppm + plen - 4, ".pfm") == 0) {
         /* linear float RGB; PFM stores rows bottom-to-top, the backbuffer's order */

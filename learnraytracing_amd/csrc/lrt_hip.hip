@@ -776,10 +776,14 @@ void free_scene(Context& c) {
     c.d_lights = nullptr;
 }
 
-int upload_scene(Context& c, const lrt_sphere* s, const lrt_material* m, int n) {
+// The device layout of a scene: float4(center, r^2), three material rows,
+// emissive ids in index order.
+int pack_scene(const lrt_sphere* s, const lrt_material* m, int n, std::vector<float4>& sph,
+               std::vector<float4>& mats, std::vector<int>& lights) {
     if (!s || !m || n < 1 || n > LRT_MAX_SPHERES) return fail(LRT_E_INVALID, "scene: need 1..LRT_MAX_SPHERES spheres");
-    std::vector<float4> sph(n), mats(3 * (size_t)n);
-    std::vector<int> lights;
+    sph.assign(n, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    mats.assign(3 * (size_t)n, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    lights.clear();
     for (int i = 0; i < n; ++i) {
         if (m[i].type < 0 || m[i].type > 2) return fail(LRT_E_INVALID, "scene: material type must be 0..2");
         const float r = s[i].radius;
@@ -795,6 +799,13 @@ int upload_scene(Context& c, const lrt_sphere* s, const lrt_material* m, int n) 
         // parallel.cpp:96: skip only if every channel <= 0
         if (!(m[i].emissive.x <= 0 && m[i].emissive.y <= 0 && m[i].emissive.z <= 0)) lights.push_back(i);
     }
+    return LRT_OK;
+}
+
+int upload_scene(Context& c, const lrt_sphere* s, const lrt_material* m, int n) {
+    std::vector<float4> sph, mats;
+    std::vector<int> lights;
+    if (const int e = pack_scene(s, m, n, sph, mats, lights)) return e;
     free_scene(c);
     LRT_HIP(hipMalloc(&c.d_sph, sizeof(float4) * n));
     LRT_HIP(hipMalloc(&c.d_mats, sizeof(float4) * 3 * n));
@@ -1457,6 +1468,47 @@ int camera_default(int w, int h, lrt_camera* out) {   // parallel.cpp:299-307
     return camera_make(L3(0, 2, 3), L3(0, 0, 0), L3(0, 1, 0), 60.0f, (float)w / (float)h, 0.1f, 3.0f, out);
 }
 
+
+// lrt_scatter_eval's case i: Scatter (lrt_trace.h, parallel.cpp:78-196) of material ids[i]
+// for the ray rays[6i..] (through the Ray ctor) at the hit recs[7i..] under RNG state seeds[i].
+template <bool kBvh>
+LRT_DEV void scatter_case(const SceneView& sc, int i, const int* ids, const float* rays, const float* recs,
+                          const uint32_t* seeds, float* out, int* ret, int* counted, uint32_t* state) {
+    const Ray r = make_ray(f3(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]),
+                           f3(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]));
+    Hit rec;
+    rec.pos = f3(recs[7 * i], recs[7 * i + 1], recs[7 * i + 2]);
+    rec.normal = f3(recs[7 * i + 3], recs[7 * i + 4], recs[7 * i + 5]);
+    rec.t = recs[7 * i + 6];
+    const Material mat = load_material(sc.mats, ids[i]);
+    uint32_t rng = seeds[i];
+    int rays_ = 0;
+    F3 att = f3(0.0f, 0.0f, 0.0f), lightE = f3(0.0f, 0.0f, 0.0f);
+    Ray sc_ray;
+    sc_ray.orig = sc_ray.dir = f3(0.0f, 0.0f, 0.0f);
+    const bool ok = Scatter<kBvh>(mat, r, rec, att, sc_ray, lightE, rays_, rng, sc);
+    const F3 v[4] = {att, sc_ray.orig, sc_ray.dir, lightE};
+    for (int k = 0; k < 4; ++k) {
+        out[12 * i + 3 * k] = v[k].x;
+        out[12 * i + 3 * k + 1] = v[k].y;
+        out[12 * i + 3 * k + 2] = v[k].z;
+    }
+    ret[i] = ok ? 1 : 0;
+    counted[i] = rays_;
+    state[i] = rng;
+}
+template <bool kBvh>
+__global__ __launch_bounds__(64) void scatter_probe_kernel(SceneView sc, const int* ids, const float* rays,
+                                                           const float* recs, const uint32_t* seeds, int n,
+                                                           float* out, int* ret, int* counted, uint32_t* state) {
+    __shared__ unsigned short stk[kBvhStackLevels * 64];
+    sc.pow = libm::pow_tables();   // the device's table addresses (the host filled in its own)
+    sc.bstk = stk + threadIdx.x;
+    sc.bstride = 64;
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i < n) scatter_case<kBvh>(sc, i, ids, rays, recs, seeds, out, ret, counted, state);
+}
+
 }  // namespace lrt
 
 using namespace lrt;
@@ -1727,6 +1779,101 @@ int lrt_bvh_stats(const lrt_sphere* spheres, int count, const float* rays, int n
     out[2] = mn;
     out[3] = ms;
     out[4] = bad / n;
+    return LRT_OK;
+}
+
+int lrt_scatter_eval(const lrt_sphere* spheres, const lrt_material* materials, int count, const int* ids,
+                     const float* rays, const float* recs, const uint32_t* seeds, int n, float* out, int* ret,
+                     int* counted, uint32_t* state, int on_device) {
+    if (!ids || !rays || !recs || !seeds || !out || !ret || !counted || !state || n < 0)
+        return fail(LRT_E_INVALID, "scatter probe: null argument");
+    std::vector<float4> sph, mats;
+    std::vector<int> lights;
+    if (const int e = pack_scene(spheres, materials, count, sph, mats, lights)) return e;
+    for (int i = 0; i < n; ++i)
+        if (ids[i] < 0 || ids[i] >= count) return fail(LRT_E_INVALID, "scatter probe: material id out of range");
+    if (n == 0) return LRT_OK;
+    const bool bvh = count > kBvhMinSpheres;
+    BvhHost B;
+    if (bvh) build_bvh_host(spheres, count, sph, B);
+    SceneView sc{};
+    sc.count = count;
+    sc.nlights = (int)lights.size();
+    if (lights.empty()) lights.push_back(0);   // never read (nlights = 0): keeps the copy non-empty
+    sc.pow = libm::pow_tables();   // host addresses: the probe kernel sets its own
+    sc.rnlut = nullptr;
+    sc.bv.margin = B.margin;
+    sc.bv.on = bvh ? 1 : 0;
+    sc.bv.nnodes = bvh ? (int)(B.nodes.size() / (LRT_BVH4 ? 8 : 4)) : 0;
+    sc.bv.big0 = B.big0;
+    sc.bv.nbig = B.nbig;
+    if (!on_device) {
+        sc.sph = sc.gsph = sph.data();
+        sc.mats = mats.data();
+        sc.lights = lights.data();
+        sc.bv.nodes = B.nodes.data();
+        sc.bv.lsph = B.lsph.data();
+        sc.bv.lid = B.lid.data();
+        unsigned short stk[kBvhStackLevels];
+        sc.bstk = stk;
+        sc.bstride = 1;
+        for (int i = 0; i < n; ++i) {
+            if (bvh) scatter_case<true>(sc, i, ids, rays, recs, seeds, out, ret, counted, state);
+            else scatter_case<false>(sc, i, ids, rays, recs, seeds, out, ret, counted, state);
+        }
+        return LRT_OK;
+    }
+    // device: one thread per case over device copies of everything
+    std::vector<void*> owned;
+    auto up = [&](const void* src, size_t bytes) -> void* {   // a device copy (>= 16 B), owned
+        void* d = nullptr;
+        if (hipMalloc(&d, std::max<size_t>(bytes, 16)) != hipSuccess) return nullptr;
+        owned.push_back(d);
+        if (bytes && hipMemcpy(d, src, bytes, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+        return d;
+    };
+    auto release = [&]() {
+        for (void* p : owned) (void)hipFree(p);
+    };
+    void* dd[10] = {up(sph.data(), sph.size() * sizeof(float4)), up(mats.data(), mats.size() * sizeof(float4)),
+                    up(lights.data(), lights.size() * sizeof(int)),
+                    up(B.nodes.data(), B.nodes.size() * sizeof(float4)),
+                    up(B.lsph.data(), B.lsph.size() * sizeof(float4)), up(B.lid.data(), B.lid.size() * sizeof(int)),
+                    up(ids, sizeof(int) * n), up(rays, sizeof(float) * 6 * n), up(recs, sizeof(float) * 7 * n),
+                    up(seeds, sizeof(uint32_t) * n)};
+    float* o_out = nullptr;
+    int *o_ret = nullptr, *o_cnt = nullptr;
+    uint32_t* o_st = nullptr;
+    if (hipMalloc(&o_out, sizeof(float) * 12 * n) == hipSuccess) owned.push_back(o_out);
+    if (hipMalloc(&o_ret, sizeof(int) * n) == hipSuccess) owned.push_back(o_ret);
+    if (hipMalloc(&o_cnt, sizeof(int) * n) == hipSuccess) owned.push_back(o_cnt);
+    if (hipMalloc(&o_st, sizeof(uint32_t) * n) == hipSuccess) owned.push_back(o_st);
+    if (std::find(std::begin(dd), std::end(dd), nullptr) != std::end(dd) || !o_out || !o_ret ||
+        !o_cnt || !o_st) {
+        release();
+        return fail(LRT_E_NOMEM, "scatter probe: device allocation failed");
+    }
+    sc.sph = sc.gsph = (const float4*)dd[0];
+    sc.mats = (const float4*)dd[1];
+    sc.lights = (const int*)dd[2];
+    sc.bv.nodes = (const float4*)dd[3];
+    sc.bv.lsph = (const float4*)dd[4];
+    sc.bv.lid = (const int*)dd[5];
+    const unsigned blocks = (unsigned)((n + 63) / 64);
+    if (bvh)
+        scatter_probe_kernel<true><<<blocks, 64>>>(sc, (const int*)dd[6], (const float*)dd[7], (const float*)dd[8],
+                                                   (const uint32_t*)dd[9], n, o_out, o_ret, o_cnt, o_st);
+    else
+        scatter_probe_kernel<false><<<blocks, 64>>>(sc, (const int*)dd[6], (const float*)dd[7], (const float*)dd[8],
+                                                    (const uint32_t*)dd[9], n, o_out, o_ret, o_cnt, o_st);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(out, o_out, sizeof(float) * 12 * n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(ret, o_ret, sizeof(int) * n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(counted, o_cnt, sizeof(int) * n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(state, o_st, sizeof(uint32_t) * n, hipMemcpyDeviceToHost);
+    release();
+    if (e != hipSuccess) return fail(LRT_E_HIP, std::string("scatter probe: ") + hipGetErrorString(e));
     return LRT_OK;
 }
 

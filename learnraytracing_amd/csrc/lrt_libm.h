@@ -169,7 +169,7 @@ LRT_CONST uint64_t kExp2Tab[32] = {
     0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
 
 // The three powf tables, by pointer so a kernel can stage them in LDS (a per-lane table
-// gather from global memory is a VMEM op; see lrt_paths2.h).
+// gather from global memory is a VMEM op; trace_kernel copies them to LDS).
 struct PowTables {
     const double* invc;     // kPowLog2InvC
     const double* logc;     // kPowLog2LogC

@@ -95,7 +95,7 @@ constexpr int kRenormR = 64;
 constexpr int kRenormBytes = ((2 * kRenormR + 1) * 4 + 15) / 16 * 16;
 LRT_DEV void renorm_lut_fill(float* lut, int tid, int block) {
     for (int j = tid; j <= 2 * kRenormR; j += block) {
-        const float d = __int_as_float(0x3f800000 + j - kRenormR);
+        const float d = libm::u2f((uint32_t)(0x3f800000 + j - kRenormR));
         lut[j] = rcp_rn(sqrt_rn(d));
     }
 }
@@ -125,7 +125,7 @@ LRT_DEV Ray make_ray(F3 o, F3 d) { Ray r; r.orig = o; r.dir = normalize(d); retu
 LRT_DEV F3 renormalize(F3 y, const float* lut) {
     if (!lut) return normalize(y);
     const float d = y.x * y.x + y.y * y.y + y.z * y.z;   // length()'s sum, same order
-    const int j = __float_as_int(d) - 0x3f800000 + kRenormR;
+    const int j = libm::f2u_i(d) - 0x3f800000 + kRenormR;
     float k;
     if ((unsigned)j <= 2u * kRenormR) k = lut[j];
     else k = rcp_rn(sqrt_rn(d));
@@ -188,6 +188,7 @@ LRT_DEV F3 RandomInUnitSphere(uint32_t& s) {
 struct Material {
     F3 albedo;
     int type;
+    int id;   // the table index: the reference's `&mat == &smat` self test (parallel.cpp:98)
     F3 emissive;
     float roughness;
     F3 att;
@@ -199,7 +200,8 @@ LRT_DEV Material load_material(const float4* __restrict__ mats, int id) {
     float4 b = mats[3 * id + 2];
     Material m;
     m.albedo = f3(a.x, a.y, a.z);
-    m.type = __float_as_int(a.w);
+    m.type = libm::f2u_i(a.w);
+    m.id = id;
     m.emissive = f3(e.x, e.y, e.z);
     m.roughness = e.w;
     m.att = f3(b.x, b.y, b.z);
@@ -485,6 +487,23 @@ LRT_DEV F3 ScatterDir(const Material& mat, int matId, const Ray& r_in, const Hit
     return RandomFloat01(rng) < reflProb ? refl : refr;
 }
 
+// Scatter in the reference's shape (parallel.cpp:78-196): the attenuation, the scattered
+// Ray (its ctor normalises the direction again, maths.h:133-137), the explicit light
+// samples in outLightE, shadow rays counted in inoutRayCount; returns false where the
+// reference absorbs (Metal scattered below the surface, :147). The RNG state and the scene
+// are explicit parameters, as in the reference's own per-stream variant
+// (src/cpu/README.md:42, fragmentShader.fs.glsl:175-218). `mat.id` is the material's table
+// index, the reference's `&mat` identity.
+template <bool kBvh = false, int kNS = 0>
+LRT_DEV bool Scatter(const Material& mat, const Ray& r_in, const Hit& rec, F3& attenuation, Ray& scattered,
+                     F3& outLightE, int& inoutRayCount, uint32_t& rng, const SceneView& sc) {
+    const F3 X = ScatterDir<kBvh, kNS>(mat, mat.id, r_in, rec, outLightE, inoutRayCount, rng, sc);
+    scattered.orig = rec.pos;
+    scattered.dir = renormalize(normalize(X), sc.rnlut);   // Ray(rec.pos, normalize(X))
+    attenuation = mat.att;                                  // albedo, or (1, 1, 1) for Dielectric (:192)
+    return mat.type != 1 || dot(scattered.dir, rec.normal) > 0.0f;
+}
+
 // Trace (parallel.cpp:200-227) as a loop. Scatter events are pushed on a per-lane
 // stack of (matE + lightE, material id); the fold T = E + att * T from the leaf
 // outwards reproduces the recursion's rounding exactly. maxDepth scatter events at
@@ -539,21 +558,18 @@ LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const S
             feat[1] = rec.pos;
             feat[2] = mat.albedo;
         }
-        if (depth < maxDepth) {   // :212
-            F3 lightE;
-            const F3 X = ScatterDir<kBvh, kNS>(mat, id, r, rec, lightE, inoutRayCount, rng, sc);
+        F3 lightE, attenuation;
+        Ray scattered;
+        // :212 -- the attenuation is the material's `att` row, which the fold reads back by id
+        if (depth < maxDepth && Scatter<kBvh, kNS>(mat, r, rec, attenuation, scattered, lightE, inoutRayCount, rng, sc)) {
             sec_count(sc, kSecPost);
-            const F3 dir = renormalize(normalize(X), sc.rnlut);
-            if (mat.type != 1 || dot(dir, rec.normal) > 0.0f) {   // Metal absorbs (:147)
-                if (ndl && prevLambert) matE = f3(0.0f, 0.0f, 0.0f);
-                prevLambert = mat.type == 0;
-                F3 e = matE + lightE;
-                put(depth, make_float4(e.x, e.y, e.z, __int_as_float(id)));
-                ++depth;
-                r.orig = rec.pos;
-                r.dir = dir;
-                continue;
-            }
+            if (ndl && prevLambert) matE = f3(0.0f, 0.0f, 0.0f);
+            prevLambert = mat.type == 0;
+            F3 e = matE + lightE;
+            put(depth, make_float4(e.x, e.y, e.z, __int_as_float(id)));
+            ++depth;
+            r = scattered;
+            continue;
         }
         leaf = matE;
         break;

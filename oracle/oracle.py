@@ -87,6 +87,7 @@ def ref(n: int = 9):
         lib.ref_hit_sphere.argtypes = [_P, _P, _P, ctypes.c_float, ctypes.c_float, _P]
         lib.ref_hit_world.argtypes = [_P, _P, ctypes.c_float, ctypes.c_float, _P]
         lib.ref_trace.argtypes = [_P, _P, ctypes.c_int, ctypes.c_uint32, _P]
+        lib.ref_scatter.argtypes = [ctypes.c_int, _P, _P, ctypes.c_uint32, _P, _P, _P]
         lib.ref_draw_test.argtypes = [ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]
         _refs[n] = lib
     return _refs[n]

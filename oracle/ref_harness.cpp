@@ -232,6 +232,35 @@ int ref_trace(const float* o, const float* d, int depth, uint32_t seed, float* o
     return rays;
 }
 
+// One reference Scatter() (parallel.cpp:78-196) of the static scene's material `id` (its
+// own table entry, so the `&mat == &smat` self test sees the address it expects) under
+// an explicit RNG state. ray: o, d (through the Ray ctor); rec: pos, normal, t.
+// out12: attenuation, scattered orig, scattered dir, lightE. Returns Scatter's bool;
+// *rays = counted shadow rays, *state = s_RndState after.
+int ref_scatter(int id, const float* ray, const float* rec, uint32_t seed, float* out12, int* rays,
+                uint32_t* state) {
+    Ray r(float3(ray[0], ray[1], ray[2]), float3(ray[3], ray[4], ray[5]));
+    Hit h;
+    h.pos = float3(rec[0], rec[1], rec[2]);
+    h.normal = float3(rec[3], rec[4], rec[5]);
+    h.t = rec[6];
+    float3 att(0, 0, 0), lightE(0, 0, 0);
+    Ray scattered(float3(0, 0, 0), float3(0, 0, 1));
+    scattered.dir = float3(0, 0, 0);
+    int n = 0;
+    s_RndState = seed;
+    const bool ok = Scatter(s_SphereMats[id], r, h, att, scattered, lightE, n);
+    const float3* v[4] = {&att, &scattered.orig, &scattered.dir, &lightE};
+    for (int k = 0; k < 4; ++k) {
+        out12[3 * k] = v[k]->x;
+        out12[3 * k + 1] = v[k]->y;
+        out12[3 * k + 2] = v[k]->z;
+    }
+    *rays = n;
+    *state = s_RndState;
+    return ok ? 1 : 0;
+}
+
 // ---- frame renderers ----------------------------------------------------------
 // Mode R: TraceRowJob(0, H) once per frame from the global stream (s_RndState = 1 at
 // the start of frame0's call only when reset != 0). buf: w*h*4 floats, caller-zeroed.
