@@ -163,8 +163,9 @@ def main():
     ap.add_argument("--scene-global", action="store_true", help="read spheres from global memory, not LDS")
     ap.add_argument("--reserve-cus", type=int, default=None,
                     help="CUs the render stream leaves free for other streams (default 0)")
-    ap.add_argument("--kernel", choices=["auto", "v0", "v3", "wf"], default="auto",
-                    help="auto: the library's policy (v0); v3: path regeneration; wf: wavefront (A/B)")
+    ap.add_argument("--kernel", choices=["auto", "v0", "v3", "wf", "pool"], default="auto",
+                    help="auto: the library's policy; v0: frame lanes; v3: path regeneration; wf: wavefront; "
+                         "pool: sample-pool regeneration (A/B)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -222,7 +223,7 @@ def main():
     rb = H if shards == 1 else args.row_block
     max_rows = max_shard_rows(H, rb, shards)
     rows = shard_rows(H, rb, shards, rank)
-    flags = (1 if args.scene_global else 0) | {"auto": 0, "v0": 2, "v3": 128, "wf": 256}[args.kernel]
+    flags = (1 if args.scene_global else 0) | {"auto": 0, "v0": 2, "v3": 128, "wf": 256, "pool": 512}[args.kernel]
     job = lrt.Job(width=W, height=H, frame0=0, frames=spp_total, max_depth=D, row_block=rb,
                   row_period=shards, row_phase=rank, row_count=rows, flags=flags)
     dev = torch.device("cuda", torch.cuda.current_device())

@@ -121,6 +121,11 @@ typedef struct lrt_render_desc {
                                 compacted queues, frame planes merged in order. No
                                 lrt_features.                                          */
 
+#define LRT_F_POOL 512       /* v5 kernel: the v0 loop with sample-pool regeneration: a lane
+                                whose path ends takes the wave's next pixel-sample at once;
+                                colours are lerped in frame order per pixel when the pool
+                                is done. No lrt_features.                             */
+
 /* ---- the reference API (parallel.h:6-8) ---------------------------------- */
 
 /* InitializeTest (parallel.cpp:231-235): binds the calling thread's current HIP device,
@@ -241,6 +246,11 @@ int lrt_libm_eval_device(int kind, const float* d_in, float* d_out, long long n)
  * the linear scan (0 by construction): closest hit (id and t), and the bounded shadow-ray
  * traversal for the scan's winner and for one other sphere per ray. */
 int lrt_bvh_stats(const lrt_sphere* spheres, int count, const float* rays, int n, double* out);
+/* Closest hit of n rays (6 floats each; d normalised as the Ray ctor does) through the BVH
+ * of the given scene: ids[i] (-1: miss) and ts[i]. mode 0: host build of the per-lane
+ * traversal; 1: the same on the device (one thread per ray); 2: the device's packet
+ * (wave-coherent) traversal over each wave's 64 rays. Host pointers; blocking. */
+int lrt_bvh_eval(const lrt_sphere* spheres, int count, const float* rays, int n, int* ids, float* ts, int mode);
 
 /* Scatter probe (no render): the device Scatter in the reference's shape (lrt_trace.h;
  * parallel.cpp:78-196 `bool Scatter(mat, r_in, rec, attenuation, scattered, outLightE,
@@ -250,8 +260,8 @@ int lrt_bvh_stats(const lrt_sphere* spheres, int count, const float* rays, int n
  * out[12i..] = attenuation, scattered origin, scattered direction, outLightE; ret[i] =
  * Scatter's result (0: absorbed); counted[i] = shadow rays counted; state[i] = the RNG
  * state after. Scenes above 16 spheres trace shadow rays through the BVH. on_device = 0
- * runs the host build of the same code, 1 one thread per case on the current device.
- * Host pointers either way; blocking. */
+ * runs the host build of the same code, 1 one thread per case on the current device, 2
+ * the same with the packet (wave-coherent) shadow traversal. Host pointers; blocking. */
 int lrt_scatter_eval(const lrt_sphere* spheres, const lrt_material* materials, int count,
                      const int* ids, const float* rays, const float* recs, const uint32_t* seeds,
                      int n, float* out, int* ret, int* counted, uint32_t* state, int on_device);

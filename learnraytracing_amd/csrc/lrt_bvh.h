@@ -79,7 +79,7 @@ struct SlabRay {
 };
 LRT_DEV SlabRay MakeSlabRay(const F3& o, const F3& d, float margin) {
     SlabRay r;
-    r.inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    r.inv = f3(rcp_rn(d.x), rcp_rn(d.y), rcp_rn(d.z));   // = 1.0f / d (lrt_trace.h), shorter
     r.oi = f3(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
     const float mi = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.inv.x), __builtin_fabsf(r.inv.y)),
                                      __builtin_fabsf(r.inv.z));
@@ -107,6 +107,11 @@ struct BvhStats { int nodes = 0, spheres = 0; };   // host diagnostics (lrt_bvh_
 // that has only shrunk since, so skipping the re-test is conservative.
 #ifndef LRT_BVH4
 #define LRT_BVH4 1
+#endif
+// LRT_BVH_PRELOAD: a node's 8 float4 are loaded at the top of the iteration, in one round
+// trip, instead of each child's pair after the previous child's box and leaf tests.
+#ifndef LRT_BVH_PRELOAD
+#define LRT_BVH_PRELOAD 0
 #endif
 #ifndef LRT_BVH_CH_RETEST   // closest hit: re-test popped children against the shrunk bestT (A/B)
 #define LRT_BVH_CH_RETEST 0
@@ -250,25 +255,72 @@ LRT_DEV bool ShadowReachesLightBVH2(const F3& o, const F3& d, int li, const floa
 }
 
 
+// Traversal knobs (A/B builds; defaults are the measured best):
+//  LRT_BVH_LAZY_ID   the leaf loop keeps the winner's leaf-array position and reads original
+//                    indices only on an exact tie and once at the end (no dependent id load
+//                    per tested sphere);
+//  LRT_BVH_SLAB_SPLIT the traversal loop is instantiated for each slab form and chosen once
+//                    per ray, instead of a (nearly always uniform) branch per child;
+//  LRT_BVH_LEAF_BATCH a leaf's sphere loads (up to kLeafBatch) are issued together before
+//                    the tests, one round trip instead of one per sphere.
+#ifndef LRT_BVH_LAZY_ID
+#define LRT_BVH_LAZY_ID 1
+#endif
+#ifndef LRT_BVH_SLAB_SPLIT
+#define LRT_BVH_SLAB_SPLIT 1
+#endif
+#ifndef LRT_BVH_LEAF_BATCH
+#define LRT_BVH_LEAF_BATCH 0
+#endif
+constexpr int kLeafBatch = 6;   // the build's default leaf size (kBvhLeaf); longer leaves loop on
+
+template <int kForm>   // 0: SlabTest4's runtime choice, 1: FMA form, 2: subtract-multiply form
+LRT_DEV void SlabTestK(const float4& mn, const float4& mx, const F3& o, const SlabRay& sr, float& tn, float& tf) {
+    if (kForm == 1) SlabTestFma(mn, mx, sr.inv, sr.oi, tn, tf);
+    else if (kForm == 2) SlabTest(mn, mx, o, sr.inv, tn, tf);
+    else SlabTest4(mn, mx, o, sr, tn, tf);
+}
+
+// Calls f(position, sphere) for the cnt leaf spheres at lsph[ref ...], their loads issued
+// together (LRT_BVH_LEAF_BATCH).
+template <class F>
+LRT_DEV void ForLeafSpheres(const float4* lsph, int ref, int cnt, F&& f) {
+    if (LRT_BVH_LEAF_BATCH) {
+        float4 sb[kLeafBatch];
+#pragma unroll
+        for (int j = 0; j < kLeafBatch; ++j)
+            if (j < cnt) sb[j] = lsph[ref + j];
+#pragma unroll
+        for (int j = 0; j < kLeafBatch; ++j)
+            if (j < cnt) f(ref + j, sb[j]);
+        for (int j = kLeafBatch; j < cnt; ++j) f(ref + j, lsph[ref + j]);
+    } else {
+        for (int j = 0; j < cnt; ++j) f(ref + j, lsph[ref + j]);
+    }
+}
+
 // 4-wide ClosestHitBVH: same leaf arithmetic, (cand, id) minimum and conservative culling.
-LRT_DEV int ClosestHitBVH4(const F3& o, const F3& d, const BvhView& bv, float& tOut, unsigned short* stk, int stride,
-                           BvhStats* st = nullptr) {
-    const SlabRay sr = MakeSlabRay(o, d, bv.margin);
+template <int kForm>
+LRT_DEV int ClosestHitBVH4Impl(const F3& o, const F3& d, const SlabRay& sr, const BvhView& bv, float& tOut,
+                               unsigned short* stk, int stride, BvhStats* st) {
     float bestT = kMaxT;
-    int best = -1;
-    auto leaf = [&](int ref, int cnt) {
-        if (st) st->spheres += cnt;
-        for (int j = 0; j < cnt; ++j) {
-            const float4 s = bv.lsph[ref + j];
-            const F3 rs = f3(s.x, s.y, s.z) - o;                       // maths.cpp:54-59
-            const float rsProj = dot(rs, d);
-            const float ifHit = dot(rs, rs) - rsProj * rsProj - s.w;
-            if (ifHit < 0.0f) {
-                const float halfCut = sqrt_rn(-ifHit);
-                const float t1 = rsProj - halfCut;
-                const float t2 = rsProj + halfCut;
-                const float cand = t1 > kMinT ? t1 : (t2 > kMinT ? t2 : __builtin_inff());
-                const int id = bv.lid[ref + j];
+    int best = -1;   // LRT_BVH_LAZY_ID: the winner's position in lsph, else its original index
+    auto test = [&](int pos, const float4& s) {
+        const F3 rs = f3(s.x, s.y, s.z) - o;                       // maths.cpp:54-59
+        const float rsProj = dot(rs, d);
+        const float ifHit = dot(rs, rs) - rsProj * rsProj - s.w;
+        if (ifHit < 0.0f) {
+            const float halfCut = sqrt_rn(-ifHit);
+            const float t1 = rsProj - halfCut;
+            const float t2 = rsProj + halfCut;
+            const float cand = t1 > kMinT ? t1 : (t2 > kMinT ? t2 : __builtin_inff());
+            if (LRT_BVH_LAZY_ID) {
+                if (cand < bestT || (cand == bestT && best >= 0 && bv.lid[pos] < bv.lid[best])) {
+                    bestT = cand;
+                    best = pos;
+                }
+            } else {
+                const int id = bv.lid[pos];
                 if (cand < bestT || (cand == bestT && best >= 0 && id < best)) {
                     bestT = cand;
                     best = id;
@@ -276,26 +328,32 @@ LRT_DEV int ClosestHitBVH4(const F3& o, const F3& d, const BvhView& bv, float& t
             }
         }
     };
+    auto leaf = [&](int ref, int cnt) {
+        if (st) st->spheres += cnt;
+        ForLeafSpheres(bv.lsph, ref, cnt, test);
+    };
     leaf(bv.big0, bv.nbig);
-    if (bv.nnodes == 0) {
-        tOut = bestT;
-        return best;
-    }
-    int sp = 0, cur = 0, msk = 0xF;
-    for (;;) {
+    int sp = 0, cur = 0, msk = bv.nnodes == 0 ? 0 : 0xF;
+    while (msk) {
         if (st) st->nodes += 1;
         const float mb = bv.margin + sr.mo + 1e-5f * bestT;
         const float mbase = bv.margin + sr.mo;
-        int next = -1, rem = 0;
+        int next = -1, rem = 0, nextRef = 0;
         float nearT = __builtin_inff();
+        float4 nd[8];
+        if (LRT_BVH_PRELOAD) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) nd[k] = bv.nodes[8 * cur + k];
+        }
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             if (!((msk >> c) & 1)) continue;
-            const float4 lo = bv.nodes[8 * cur + 2 * c], hi = bv.nodes[8 * cur + 2 * c + 1];
+            const float4 lo = LRT_BVH_PRELOAD ? nd[2 * c] : bv.nodes[8 * cur + 2 * c];
+            const float4 hi = LRT_BVH_PRELOAD ? nd[2 * c + 1] : bv.nodes[8 * cur + 2 * c + 1];
             const int cnt = lrt::libm::f2u_i(hi.w);
             if (cnt < 0) continue;
             float tn, tf;
-            SlabTest4(lo, hi, o, sr, tn, tf);
+            SlabTestK<kForm>(lo, hi, o, sr, tn, tf);
             const float m = __builtin_fmaf(1e-5f, __builtin_fabsf(tf), mbase);   // a margin: rounding is immaterial
             const float tfm = tf + m;   // (tn <= tf + m, tn <= bestT + mb, tf + m >= kMinT)
             if (!(tn <= __builtin_fminf(tfm, bestT + mb) && tfm >= kMinT)) continue;
@@ -306,6 +364,7 @@ LRT_DEV int ClosestHitBVH4(const F3& o, const F3& d, const BvhView& bv, float& t
                 if (tn < nearT) {
                     nearT = tn;
                     next = c;
+                    nextRef = lrt::libm::f2u_i(lo.w);
                 }
             }
         }
@@ -315,7 +374,7 @@ LRT_DEV int ClosestHitBVH4(const F3& o, const F3& d, const BvhView& bv, float& t
                 stk[sp * stride] = (unsigned short)((cur << 4) | rem);
                 ++sp;
             }
-            cur = lrt::libm::f2u_i(bv.nodes[8 * cur + 2 * next].w);
+            cur = nextRef;
             msk = 0xF;
         } else {
             if (sp == 0) break;
@@ -336,44 +395,59 @@ LRT_DEV int ClosestHitBVH4(const F3& o, const F3& d, const BvhView& bv, float& t
         }
     }
     tOut = bestT;
-    return best;
+    return (LRT_BVH_LAZY_ID && best >= 0) ? bv.lid[best] : best;
 }
 
-LRT_DEV bool ShadowReachesLightBVH4(const F3& o, const F3& d, int li, const float4& lightSph, const BvhView& bv,
-                                    unsigned short* stk, int stride) {
-    const float candL = SphereCand(o, d, lightSph);
-    if (!(candL < kMaxT)) return false;   // the light is not hit at all (closestT starts at kMaxT)
-    auto beats = [&](float c, int id) { return c < candL || (c == candL && id < li); };
-    for (int j = 0; j < bv.nbig; ++j)
-        if (beats(SphereCand(o, d, bv.lsph[bv.big0 + j]), bv.lid[bv.big0 + j])) return false;
-    if (bv.nnodes == 0) return true;
+LRT_DEV int ClosestHitBVH4(const F3& o, const F3& d, const BvhView& bv, float& tOut, unsigned short* stk, int stride,
+                           BvhStats* st = nullptr) {
     const SlabRay sr = MakeSlabRay(o, d, bv.margin);
+    if (!LRT_BVH_SLAB_SPLIT) return ClosestHitBVH4Impl<0>(o, d, sr, bv, tOut, stk, stride, st);
+    if (sr.fma) return ClosestHitBVH4Impl<1>(o, d, sr, bv, tOut, stk, stride, st);
+    return ClosestHitBVH4Impl<2>(o, d, sr, bv, tOut, stk, stride, st);
+}
+
+template <int kForm>
+LRT_DEV bool ShadowReachesLightBVH4Impl(const F3& o, const F3& d, int li, float candL, const SlabRay& sr,
+                                        const BvhView& bv, unsigned short* stk, int stride) {
+    // (cand, index) beats the light's (candL, li); the index is read only on an exact tie
+    auto beats = [&](float c, int pos) { return c < candL || (c == candL && bv.lid[pos] < li); };
+    bool blocked = false;
+    auto test = [&](int pos, const float4& s) { blocked = blocked || beats(SphereCand(o, d, s), pos); };
+    for (int j = 0; j < bv.nbig; ++j)
+        if (beats(SphereCand(o, d, bv.lsph[bv.big0 + j]), bv.big0 + j)) return false;
+    if (bv.nnodes == 0) return true;
     const float mb = bv.margin + sr.mo + 1e-5f * candL;
     const float mbase = bv.margin + sr.mo;
     int sp = 0, cur = 0, msk = 0xF;
     for (;;) {
-        int next = -1, rem = 0;
+        int next = -1, rem = 0, nextRef = 0;
         float nearT = __builtin_inff();
+        float4 nd[8];
+        if (LRT_BVH_PRELOAD) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) nd[k] = bv.nodes[8 * cur + k];
+        }
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             if (!((msk >> c) & 1)) continue;
-            const float4 lo = bv.nodes[8 * cur + 2 * c], hi = bv.nodes[8 * cur + 2 * c + 1];
+            const float4 lo = LRT_BVH_PRELOAD ? nd[2 * c] : bv.nodes[8 * cur + 2 * c];
+            const float4 hi = LRT_BVH_PRELOAD ? nd[2 * c + 1] : bv.nodes[8 * cur + 2 * c + 1];
             const int cnt = lrt::libm::f2u_i(hi.w);
             if (cnt < 0) continue;
             float tn, tf;
-            SlabTest4(lo, hi, o, sr, tn, tf);
+            SlabTestK<kForm>(lo, hi, o, sr, tn, tf);
             const float m = __builtin_fmaf(1e-5f, __builtin_fabsf(tf), mbase);   // a margin: rounding is immaterial
             const float tfm = tf + m;   // (tn <= tf + m, tn <= candL + mb, tf + m >= kMinT)
             if (!(tn <= __builtin_fminf(tfm, candL + mb) && tfm >= kMinT)) continue;
             if (cnt > 0) {
-                const int ref = lrt::libm::f2u_i(lo.w);
-                for (int j = 0; j < cnt; ++j)
-                    if (beats(SphereCand(o, d, bv.lsph[ref + j]), bv.lid[ref + j])) return false;
+                ForLeafSpheres(bv.lsph, lrt::libm::f2u_i(lo.w), cnt, test);
+                if (blocked) return false;
             } else {
                 rem |= 1 << c;
                 if (tn < nearT) {
                     nearT = tn;
                     next = c;
+                    nextRef = lrt::libm::f2u_i(lo.w);
                 }
             }
         }
@@ -383,7 +457,7 @@ LRT_DEV bool ShadowReachesLightBVH4(const F3& o, const F3& d, int li, const floa
                 stk[sp * stride] = (unsigned short)((cur << 4) | rem);
                 ++sp;
             }
-            cur = lrt::libm::f2u_i(bv.nodes[8 * cur + 2 * next].w);
+            cur = nextRef;
             msk = 0xF;
         } else {
             if (sp == 0) break;
@@ -406,13 +480,313 @@ LRT_DEV bool ShadowReachesLightBVH4(const F3& o, const F3& d, int li, const floa
     return true;
 }
 
-// The layout the host built (build_bvh_host): 4-wide unless LRT_BVH4=0.
+LRT_DEV bool ShadowReachesLightBVH4(const F3& o, const F3& d, int li, const float4& lightSph, const BvhView& bv,
+                                    unsigned short* stk, int stride) {
+    const float candL = SphereCand(o, d, lightSph);
+    if (!(candL < kMaxT)) return false;   // the light is not hit at all (closestT starts at kMaxT)
+    const SlabRay sr = MakeSlabRay(o, d, bv.margin);
+    if (!LRT_BVH_SLAB_SPLIT) return ShadowReachesLightBVH4Impl<0>(o, d, li, candL, sr, bv, stk, stride);
+    if (sr.fma) return ShadowReachesLightBVH4Impl<1>(o, d, li, candL, sr, bv, stk, stride);
+    return ShadowReachesLightBVH4Impl<2>(o, d, li, candL, sr, bv, stk, stride);
+}
+
+// Two queries from one origin in ONE traversal loop (the pool kernel's bounce step,
+// lrt_pool.h): first the deferred shadow ray of the last scatter's last light (ds, light
+// li, when hasS), then the next bounce ray's closest hit (db). A lane without a shadow ray
+// starts on its bounce ray at once, so a wave runs max over lanes of (shadow + bounce)
+// node iterations instead of max(shadow) + max(bounce) in two separate loops.
+// The shadow query is the closest-hit query with its bound preset to the light's own
+// candidate, (candL, li): a sphere that would replace it is exactly one that beats the
+// light, `HitWorld(shadow ray) && hitID == li` is false (parallel.cpp:122-123), and the
+// query ends there. Same per-sphere arithmetic, conservative culling and (cand, index)
+// order as ClosestHitBVH4 / ShadowReachesLightBVH4, so both answers are bit-identical.
+LRT_DEV int ClosestHitDualBVH4(const F3& o, const F3& db, bool hasS, const F3& ds, int li, const float4& lightSph,
+                               const BvhView& bv, float& tOut, bool& lit, unsigned short* stk, int stride) {
+    float candL = kMaxT;
+    if (hasS) candL = SphereCand(o, ds, lightSph);
+    bool sh = candL < kMaxT;   // a light that is not hit at all is not lit (closestT starts at kMaxT)
+    lit = false;
+    F3 d = sh ? ds : db;
+    SlabRay sr = MakeSlabRay(o, d, bv.margin);
+    float bestT = sh ? candL : kMaxT;
+    int best = sh ? -2 : -1;   // position in lsph; -2: the light (index li); -1: nothing yet
+    auto test = [&](int pos, const float4& s) {
+        const F3 rs = f3(s.x, s.y, s.z) - o;                       // maths.cpp:54-59
+        const float rsProj = dot(rs, d);
+        const float ifHit = dot(rs, rs) - rsProj * rsProj - s.w;
+        if (ifHit < 0.0f) {
+            const float halfCut = sqrt_rn(-ifHit);
+            const float t1 = rsProj - halfCut;
+            const float t2 = rsProj + halfCut;
+            const float cand = t1 > kMinT ? t1 : (t2 > kMinT ? t2 : __builtin_inff());
+            if (cand < bestT ||
+                (cand == bestT && best != -1 && bv.lid[pos] < (best >= 0 ? bv.lid[best] : li))) {
+                bestT = cand;
+                best = pos;
+            }
+        }
+    };
+    for (int j = 0; j < bv.nbig; ++j) test(bv.big0 + j, bv.lsph[bv.big0 + j]);
+    int sp = 0, cur = 0, msk = bv.nnodes == 0 ? 0 : 0xF;
+    for (;;) {
+        bool qdone = msk == 0 || (sh && best != -2);   // stack exhausted, or the light is beaten
+        if (!qdone) {
+            const float mb = bv.margin + sr.mo + 1e-5f * bestT;
+            const float mbase = bv.margin + sr.mo;
+            int next = -1, rem = 0, nextRef = 0;
+            float nearT = __builtin_inff();
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                if (!((msk >> c) & 1)) continue;
+                const float4 lo = bv.nodes[8 * cur + 2 * c], hi = bv.nodes[8 * cur + 2 * c + 1];
+                const int cnt = lrt::libm::f2u_i(hi.w);
+                if (cnt < 0) continue;
+                float tn, tf;
+                SlabTest4(lo, hi, o, sr, tn, tf);
+                const float m = __builtin_fmaf(1e-5f, __builtin_fabsf(tf), mbase);   // a margin
+                const float tfm = tf + m;   // (tn <= tf + m, tn <= bestT + mb, tf + m >= kMinT)
+                if (!(tn <= __builtin_fminf(tfm, bestT + mb) && tfm >= kMinT)) continue;
+                if (cnt > 0) {
+                    const int ref = lrt::libm::f2u_i(lo.w);
+                    for (int j = 0; j < cnt; ++j) test(ref + j, bv.lsph[ref + j]);
+                } else {
+                    rem |= 1 << c;
+                    if (tn < nearT) {
+                        nearT = tn;
+                        next = c;
+                        nextRef = lrt::libm::f2u_i(lo.w);
+                    }
+                }
+            }
+            if (next >= 0) {
+                rem &= ~(1 << next);
+                if (rem) {
+                    stk[sp * stride] = (unsigned short)((cur << 4) | rem);
+                    ++sp;
+                }
+                cur = nextRef;
+                msk = 0xF;
+            } else if (sp == 0) {
+                msk = 0;   // this query's traversal is complete
+            } else {   // popped children descend without a second box test (as ClosestHitBVH4)
+                --sp;
+                const int e = stk[sp * stride];
+                cur = e >> 4;
+                msk = e & 0xF;
+                const int c = __builtin_ctz(msk);
+                msk &= msk - 1;
+                if (msk) {
+                    stk[sp * stride] = (unsigned short)((cur << 4) | msk);
+                    ++sp;
+                }
+                cur = lrt::libm::f2u_i(bv.nodes[8 * cur + 2 * c].w);
+                msk = 0xF;
+            }
+            qdone = msk == 0 || (sh && best != -2);
+        }
+        if (qdone) {
+            if (!sh) break;
+            lit = best == -2;   // nothing beat the light
+            // the bounce ray's closest hit from the same origin
+            sh = false;
+            d = db;
+            sr = MakeSlabRay(o, d, bv.margin);
+            bestT = kMaxT;
+            best = -1;
+            for (int j = 0; j < bv.nbig; ++j) test(bv.big0 + j, bv.lsph[bv.big0 + j]);
+            sp = 0;
+            cur = 0;
+            msk = bv.nnodes == 0 ? 0 : 0xF;
+        }
+    }
+    tOut = bestT;
+    return best >= 0 ? bv.lid[best] : -1;
+}
+
+// ---- packet (wave-coherent) traversal ----------------------------------------------
+// For rays that start together and point the same way -- a wave's camera rays (its 64
+// lanes are a few adjacent pixels' samples) and the shadow rays from their first hits --
+// every active lane walks the SAME node sequence: a child is entered when any lane's box
+// test passes (ballot), the near-first order follows the first active lane, and the stack
+// is wave-uniform. Node and leaf-sphere data come through scalar loads (one per wave, in
+// SGPRs), the loop control is scalar, and no lane waits on another's divergent path.
+// Exactness is unchanged: a lane tests every sphere its own conservative culling keeps (a
+// superset is harmless -- the (cand, index) minimum over more real spheres is the same),
+// with the same per-sphere arithmetic. Device only; the caller checks that every active
+// lane has the FMA slab form. LRT_PACKET_DEPTH: scatter events below which a path's rays
+// go this way (0: never).
+#ifndef LRT_PACKET_DEPTH
+#define LRT_PACKET_DEPTH 1
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
+#define LRT_PACKET_AVAILABLE 1
+typedef const __attribute__((address_space(4))) float4* CF4Ptr;
+__device__ __forceinline__ int wave_first(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ float wave_first(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
+
+__device__ __forceinline__ int ClosestHitPacket(const F3& o, const F3& d, const SlabRay& sr, const BvhView& bv,
+                                                float& tOut, unsigned short* stk, int stride) {
+    const CF4Ptr nodes = (CF4Ptr)bv.nodes;
+    const CF4Ptr lsph = (CF4Ptr)bv.lsph;
+    float bestT = kMaxT;
+    int best = -1;   // the winner's position in lsph
+    auto test = [&](int pos, const float4& s) {
+        const F3 rs = f3(s.x, s.y, s.z) - o;                       // maths.cpp:54-59
+        const float rsProj = dot(rs, d);
+        const float ifHit = dot(rs, rs) - rsProj * rsProj - s.w;
+        if (ifHit < 0.0f) {
+            const float halfCut = sqrt_rn(-ifHit);
+            const float t1 = rsProj - halfCut;
+            const float t2 = rsProj + halfCut;
+            const float cand = t1 > kMinT ? t1 : (t2 > kMinT ? t2 : __builtin_inff());
+            if (cand < bestT || (cand == bestT && best >= 0 && bv.lid[pos] < bv.lid[best])) {
+                bestT = cand;
+                best = pos;
+            }
+        }
+    };
+    for (int j = 0; j < bv.nbig; ++j) test(bv.big0 + j, lsph[bv.big0 + j]);
+    int sp = 0, cur = 0, msk = bv.nnodes == 0 ? 0 : 0xF;
+    while (msk) {
+        const float mb = bv.margin + sr.mo + 1e-5f * bestT;
+        const float mbase = bv.margin + sr.mo;
+        int next = -1, rem = 0, nextRef = 0;
+        float nearT = __builtin_inff();
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (!((msk >> c) & 1)) continue;
+            const float4 lo = nodes[8 * cur + 2 * c], hi = nodes[8 * cur + 2 * c + 1];
+            const int cnt = lrt::libm::f2u_i(hi.w);
+            if (cnt < 0) continue;
+            float tn, tf;
+            SlabTestFma(lo, hi, sr.inv, sr.oi, tn, tf);
+            const float m = __builtin_fmaf(1e-5f, __builtin_fabsf(tf), mbase);
+            const float tfm = tf + m;
+            const bool hit = tn <= __builtin_fminf(tfm, bestT + mb) && tfm >= kMinT;
+            if (__ballot(hit) == 0) continue;
+            const int ref = lrt::libm::f2u_i(lo.w);
+            if (cnt > 0) {
+                if (hit)
+                    for (int j = 0; j < cnt; ++j) test(ref + j, lsph[ref + j]);
+            } else {
+                rem |= 1 << c;
+                const float k = wave_first(hit ? tn : __builtin_inff());
+                if (next < 0 || k < nearT) {
+                    nearT = k;
+                    next = c;
+                    nextRef = ref;
+                }
+            }
+        }
+        if (next >= 0) {
+            rem &= ~(1 << next);
+            if (rem) {
+                stk[sp * stride] = (unsigned short)((cur << 4) | rem);
+                ++sp;
+            }
+            cur = nextRef;
+            msk = 0xF;
+        } else {
+            if (sp == 0) break;
+            --sp;
+            const int e = wave_first((int)stk[sp * stride]);
+            cur = e >> 4;
+            msk = e & 0xF;   // re-tested against each lane's shrunk bestT
+        }
+    }
+    tOut = bestT;
+    return best >= 0 ? bv.lid[best] : -1;
+}
+
+__device__ __forceinline__ bool ShadowPacket(const F3& o, const F3& d, int li, float candL, const SlabRay& sr,
+                                             const BvhView& bv, unsigned short* stk, int stride) {
+    const CF4Ptr nodes = (CF4Ptr)bv.nodes;
+    const CF4Ptr lsph = (CF4Ptr)bv.lsph;
+    auto beats = [&](float c, int pos) { return c < candL || (c == candL && bv.lid[pos] < li); };
+    bool alive = true;   // no sphere beats the light yet
+    for (int j = 0; j < bv.nbig; ++j)
+        if (beats(SphereCand(o, d, lsph[bv.big0 + j]), bv.big0 + j)) alive = false;
+    const float mb = bv.margin + sr.mo + 1e-5f * candL;
+    const float mbase = bv.margin + sr.mo;
+    int sp = 0, cur = 0, msk = bv.nnodes == 0 ? 0 : 0xF;
+    while (msk && __ballot(alive) != 0) {
+        int next = -1, rem = 0, nextRef = 0;
+        float nearT = __builtin_inff();
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (!((msk >> c) & 1)) continue;
+            const float4 lo = nodes[8 * cur + 2 * c], hi = nodes[8 * cur + 2 * c + 1];
+            const int cnt = lrt::libm::f2u_i(hi.w);
+            if (cnt < 0) continue;
+            float tn, tf;
+            SlabTestFma(lo, hi, sr.inv, sr.oi, tn, tf);
+            const float m = __builtin_fmaf(1e-5f, __builtin_fabsf(tf), mbase);
+            const float tfm = tf + m;
+            const bool hit = alive && tn <= __builtin_fminf(tfm, candL + mb) && tfm >= kMinT;
+            if (__ballot(hit) == 0) continue;
+            const int ref = lrt::libm::f2u_i(lo.w);
+            if (cnt > 0) {
+                if (hit)
+                    for (int j = 0; j < cnt; ++j)
+                        if (beats(SphereCand(o, d, lsph[ref + j]), ref + j)) alive = false;
+            } else {
+                rem |= 1 << c;
+                const float k = wave_first(hit ? tn : __builtin_inff());
+                if (next < 0 || k < nearT) {
+                    nearT = k;
+                    next = c;
+                    nextRef = ref;
+                }
+            }
+        }
+        if (next >= 0) {
+            rem &= ~(1 << next);
+            if (rem) {
+                stk[sp * stride] = (unsigned short)((cur << 4) | rem);
+                ++sp;
+            }
+            cur = nextRef;
+            msk = 0xF;
+        } else {
+            if (sp == 0) break;
+            --sp;
+            const int e = wave_first((int)stk[sp * stride]);
+            cur = e >> 4;
+            msk = e & 0xF;   // re-tested: lanes blocked since no longer count
+        }
+    }
+    return alive;
+}
+#else
+#define LRT_PACKET_AVAILABLE 0
+#endif
+
+// The layout the host built (build_bvh_host): 4-wide unless LRT_BVH4=0. coherent: the
+// caller's active lanes are rays that start together (packet traversal when every one of
+// them takes the FMA slab form).
 LRT_DEV int ClosestHitBVH(const F3& o, const F3& d, const BvhView& bv, float& tOut, unsigned short* stk, int stride,
-                          BvhStats* st = nullptr) {
+                          BvhStats* st = nullptr, bool coherent = false) {
+#if LRT_PACKET_AVAILABLE && LRT_BVH4
+    if (coherent) {
+        const SlabRay sr = MakeSlabRay(o, d, bv.margin);
+        if (__ballot(!sr.fma) == 0) return ClosestHitPacket(o, d, sr, bv, tOut, stk, stride);
+    }
+#endif
+    (void)coherent;
     return LRT_BVH4 ? ClosestHitBVH4(o, d, bv, tOut, stk, stride, st) : ClosestHitBVH2(o, d, bv, tOut, stk, stride, st);
 }
 LRT_DEV bool ShadowReachesLightBVH(const F3& o, const F3& d, int li, const float4& lightSph, const BvhView& bv,
-                                   unsigned short* stk, int stride) {
+                                   unsigned short* stk, int stride, bool coherent = false) {
+#if LRT_PACKET_AVAILABLE && LRT_BVH4
+    if (coherent) {
+        const float candL = SphereCand(o, d, lightSph);
+        const SlabRay sr = MakeSlabRay(o, d, bv.margin);
+        if (__ballot(!sr.fma) == 0) return candL < kMaxT && ShadowPacket(o, d, li, candL, sr, bv, stk, stride);
+    }
+#endif
+    (void)coherent;
     return LRT_BVH4 ? ShadowReachesLightBVH4(o, d, li, lightSph, bv, stk, stride)
                     : ShadowReachesLightBVH2(o, d, li, lightSph, bv, stk, stride);
 }

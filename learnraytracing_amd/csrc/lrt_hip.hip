@@ -81,6 +81,7 @@ struct KernelArgs {
     int regenMin;                 // v3: ended lanes that trigger a regeneration round
     const float* lerp;            // lerpFac = (float)f / (float)(f + 1) for f < kLerpTable (parallel.cpp:262)
     float4* samp;                 // sample mode: frames planes of xc * rows colours
+    float4* colbuf;               // v5 (pool): kPoolSamples colour slots per block
 };
 constexpr int kLerpTable = 1 << 16;
 constexpr int kFixedSpheres = 9;   // the reference's kSphereCount (parallel.cpp:27)
@@ -364,6 +365,7 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
 
 }  // namespace lrt
 #include "lrt_regen.h"
+#include "lrt_pool.h"
 namespace lrt {
 // (lrt_wavefront.h follows merge_samples_kernel)
 
@@ -913,7 +915,8 @@ void secstats_dump(const unsigned long long* d_sec, hipStream_t s) {
         unsigned long long h[3 * kSecN * 16];
         (void)hipMemcpyAsync(h, d_sec, sizeof(h), hipMemcpyDeviceToHost, s);
         (void)hipStreamSynchronize(s);
-        const char* names[kSecN] = {"hit", "lambert", "shadow", "metal", "dielectric", "post", "fold", "camera", "other"};
+        const char* names[kSecN] = {"hit", "lambert", "shadow", "metal", "dielectric", "post", "fold", "camera", "other",
+                                    "hit0", "shadow0"};
         double tot = 0;
         for (int k = 0; k < kSecN; ++k)
             for (int j = 0; j < 16; ++j) tot += (double)h[3 * (k + kSecN * j) + 2];
@@ -1167,6 +1170,82 @@ int launch_regen_split(const KernelArgs& a, bool lds, int xc, int rows, int fram
     return launch_regen<MAXD, 1>(a, lds, xc, rows, s);
 }
 
+// v5 (lrt_pool.h): v0's LDS layout, queues, counters and overflow stack, plus the
+// per-block colour slots.
+template <int MAXD, int kPix>
+int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
+    constexpr int TX = PoolTile<kPix>::X, TY = PoolTile<kPix>::Y;
+    const long long ntiles = (long long)((xc + TX - 1) / TX) * ((rows + TY - 1) / TY);
+    const size_t stack = sizeof(float4) * kTraceLdsLevels * 64 + kPowTableBytes + (a.bv.on ? 0 : kRenormBytes);
+    const size_t scene = lds ? sizeof(float4) * (4 * (size_t)a.count + (size_t)(a.nlights + 3) / 4 + 1) : 0;
+    a.bvh_stack_offset = (int)(stack + scene);
+    const size_t bstk = a.bv.on ? sizeof(unsigned short) * g_ctx.bvh_stack_levels * 64 : 0;
+    const size_t ldsb = stack + scene + bstk;
+    const bool fixed = lds && !a.bv.on && a.count == kFixedSpheres;
+    const void* kern = a.bv.on ? (lds ? (const void*)pool_kernel<MAXD, true, true, kPix>
+                                      : (const void*)pool_kernel<MAXD, false, true, kPix>)
+                               : (fixed ? (const void*)pool_kernel<MAXD, true, false, kPix, kFixedSpheres>
+                                  : lds ? (const void*)pool_kernel<MAXD, true, false, kPix>
+                                        : (const void*)pool_kernel<MAXD, false, false, kPix>);
+    int per_cu = 0;
+    hipError_t e = occupancy(&per_cu, kern, 64, ldsb);
+    if (e != hipSuccess) return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
+    if (per_cu < 1) return fail(LRT_E_INVALID, "pool_kernel does not fit on a CU");
+    int cus = g_ctx.num_cus;
+    for (const auto& m : g_ctx.masked_streams)
+        if (m.first == s) cus = m.second;
+    long long blocks = std::max((long long)per_cu * cus, (long long)kV0Queues);   // a block per queue (as v0)
+    if (blocks > ntiles) blocks = ntiles;
+    const dim3 grid((unsigned)blocks);
+    a.ovf = nullptr;
+    a.colbuf = nullptr;
+    a.tiles = g_ctx.d_tiles + (size_t)(g_ctx.tiles_next++ % kQueueSlots) * kTileSetU64;
+    e = hipMallocAsync((void**)&a.colbuf, sizeof(float4) * kPoolSamples * (size_t)grid.x, s);
+    if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(pool colour slots)");
+    if (a.maxDepth > kTraceLdsLevels) {
+        const size_t gthreads = (size_t)grid.x * 64;
+        e = hipMallocAsync((void**)&a.ovf, sizeof(float4) * gthreads * (size_t)(a.maxDepth - kTraceLdsLevels), s);
+        if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(trace stack overflow)");
+    }
+#ifdef LRT_EXP_SECSTATS
+    unsigned long long* d_sec = secstats_buffer(s);
+    a.wtrace = d_sec;
+#endif
+    if (a.bv.on) {
+        if (lds) pool_kernel<MAXD, true, true, kPix><<<grid, 64, ldsb, s>>>(a);
+        else pool_kernel<MAXD, false, true, kPix><<<grid, 64, ldsb, s>>>(a);
+    } else if (fixed) {
+        pool_kernel<MAXD, true, false, kPix, kFixedSpheres><<<grid, 64, ldsb, s>>>(a);
+    } else {
+        if (lds) pool_kernel<MAXD, true, false, kPix><<<grid, 64, ldsb, s>>>(a);
+        else pool_kernel<MAXD, false, false, kPix><<<grid, 64, ldsb, s>>>(a);
+    }
+    e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "pool_kernel launch");
+    snprintf(g_last_launch, sizeof(g_last_launch),
+             "kernel=pool_kernel maxd=%d lds=%d bvh=%d pix=%d ns=%d grid=%u tasks=%lld per_cu=%d", MAXD, lds ? 1 : 0,
+             a.bv.on ? 1 : 0, kPix, fixed ? kFixedSpheres : 0, grid.x, ntiles, per_cu);
+#ifdef LRT_EXP_SECSTATS
+    secstats_dump(d_sec, s);
+#endif
+    e = hipFreeAsync(a.colbuf, s);
+    if (e != hipSuccess) return hip_fail(e, "hipFreeAsync(pool colour slots)");
+    if (a.ovf) {
+        e = hipFreeAsync(a.ovf, s);
+        if (e != hipSuccess) return hip_fail(e, "hipFreeAsync(trace stack overflow)");
+    }
+    return LRT_OK;
+}
+
+// Pixels per pool tile: a round holds kPoolSamples samples, so more frames -> fewer pixels.
+template <int MAXD>
+int launch_pool_split(const KernelArgs& a, bool lds, int xc, int rows, int frames, hipStream_t s) {
+    if (frames <= 16) return launch_pool<MAXD, 64>(a, lds, xc, rows, s);
+    if (frames <= 64) return launch_pool<MAXD, 16>(a, lds, xc, rows, s);
+    if (frames <= 256) return launch_pool<MAXD, 4>(a, lds, xc, rows, s);
+    return launch_pool<MAXD, 1>(a, lds, xc, rows, s);
+}
+
 // v4 (lrt_wavefront.h): chunks of whole pixels, maxDepth + 1 extend/shade rounds each,
 // then the chunk's frame planes merged into the window. Path state is ~100 B + 16 B per
 // recursion level per pixel-sample; chunks are sized to a 2 GB budget.
@@ -1331,13 +1410,16 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     a.lerp = g_ctx.d_lerp;
     if (d->flags & (LRT_F_V1 | LRT_F_V2S | LRT_F_V2))
         return fail(LRT_E_INVALID, "LRT_F_V1/LRT_F_V2S/LRT_F_V2 kernels were removed (use LRT_F_SIMPLE, the default)");
-    int kflags = d->flags & (LRT_F_SIMPLE | LRT_F_V3 | LRT_F_WAVEFRONT);
+    int kflags = d->flags & (LRT_F_SIMPLE | LRT_F_V3 | LRT_F_WAVEFRONT | LRT_F_POOL);
     if (kflags == 0) kflags = LRT_F_SIMPLE;
     if (want_feat && !(kflags & LRT_F_SIMPLE))
         return fail(LRT_E_INVALID, "features are implemented by the v0 kernel only");
-    if (a.ndl && !(kflags & (LRT_F_SIMPLE | LRT_F_V3 | LRT_F_WAVEFRONT)))
-        return fail(LRT_E_INVALID, "LRT_F_NO_DOUBLE_LIGHT is implemented by the v0, v3 and wavefront kernels only");
     if (kflags & LRT_F_WAVEFRONT) return launch_wavefront(a, lds, s);
+    if (kflags & LRT_F_POOL) {
+        a.colbuf = nullptr;
+        if (d->max_depth <= 8) return launch_pool_split<8>(a, lds, d->x_count, d->row_count, d->frames, s);
+        return launch_pool_split<64>(a, lds, d->x_count, d->row_count, d->frames, s);
+    }
     if (kflags & LRT_F_V3) {
         if (d->max_depth <= 8) return launch_regen_split<8>(a, lds, d->x_count, d->row_count, d->frames, s);
         return launch_regen_split<64>(a, lds, d->x_count, d->row_count, d->frames, s);
@@ -1473,7 +1555,8 @@ int camera_default(int w, int h, lrt_camera* out) {   // parallel.cpp:299-307
 // for the ray rays[6i..] (through the Ray ctor) at the hit recs[7i..] under RNG state seeds[i].
 template <bool kBvh>
 LRT_DEV void scatter_case(const SceneView& sc, int i, const int* ids, const float* rays, const float* recs,
-                          const uint32_t* seeds, float* out, int* ret, int* counted, uint32_t* state) {
+                          const uint32_t* seeds, float* out, int* ret, int* counted, uint32_t* state,
+                          bool coherent = false) {
     const Ray r = make_ray(f3(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]),
                            f3(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]));
     Hit rec;
@@ -1486,7 +1569,7 @@ LRT_DEV void scatter_case(const SceneView& sc, int i, const int* ids, const floa
     F3 att = f3(0.0f, 0.0f, 0.0f), lightE = f3(0.0f, 0.0f, 0.0f);
     Ray sc_ray;
     sc_ray.orig = sc_ray.dir = f3(0.0f, 0.0f, 0.0f);
-    const bool ok = Scatter<kBvh>(mat, r, rec, att, sc_ray, lightE, rays_, rng, sc);
+    const bool ok = Scatter<kBvh>(mat, r, rec, att, sc_ray, lightE, rays_, rng, sc, coherent);
     const F3 v[4] = {att, sc_ray.orig, sc_ray.dir, lightE};
     for (int k = 0; k < 4; ++k) {
         out[12 * i + 3 * k] = v[k].x;
@@ -1500,13 +1583,27 @@ LRT_DEV void scatter_case(const SceneView& sc, int i, const int* ids, const floa
 template <bool kBvh>
 __global__ __launch_bounds__(64) void scatter_probe_kernel(SceneView sc, const int* ids, const float* rays,
                                                            const float* recs, const uint32_t* seeds, int n,
-                                                           float* out, int* ret, int* counted, uint32_t* state) {
+                                                           float* out, int* ret, int* counted, uint32_t* state,
+                                                           int coherent) {
     __shared__ unsigned short stk[kBvhStackLevels * 64];
     sc.pow = libm::pow_tables();   // the device's table addresses (the host filled in its own)
     sc.bstk = stk + threadIdx.x;
     sc.bstride = 64;
     const int i = blockIdx.x * 64 + threadIdx.x;
-    if (i < n) scatter_case<kBvh>(sc, i, ids, rays, recs, seeds, out, ret, counted, state);
+    if (i < n) scatter_case<kBvh>(sc, i, ids, rays, recs, seeds, out, ret, counted, state, coherent != 0);
+}
+
+// lrt_bvh_eval's device side: one thread per ray, per-lane or packet traversal.
+__global__ __launch_bounds__(64) void bvh_probe_kernel(BvhView bv, const float* rays, int n, int* ids, float* ts,
+                                                       int packet) {
+    __shared__ unsigned short stk[kBvhStackLevels * 64];
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= n) return;
+    const Ray r = make_ray(f3(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]),
+                           f3(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]));
+    float t = 0.0f;
+    ids[i] = ClosestHitBVH(r.orig, r.dir, bv, t, stk + threadIdx.x, 64, nullptr, packet != 0);
+    ts[i] = t;
 }
 
 }  // namespace lrt
@@ -1769,6 +1866,23 @@ int lrt_bvh_stats(const lrt_sphere* spheres, int count, const float* rays, int n
         if (b >= 0 && !ShadowReachesLightBVH(r.orig, r.dir, b, sph[b], bv, stk, 1)) bad += 1;
         const int other = (int)(((unsigned)i * 7919u) % (unsigned)count);
         if (ShadowReachesLightBVH(r.orig, r.dir, other, sph[other], bv, stk, 1) != (b == other)) bad += 1;
+        // the two-query loop (pool kernel): this ray as the shadow ray towards `other` (and
+        // towards the winner), the next ray's direction from the same origin as the bounce ray
+        if (LRT_BVH4) {
+            const int i2 = (i + 1) % n;
+            const Ray r2 = make_ray(r.orig, f3(rays[6 * i2 + 3], rays[6 * i2 + 4], rays[6 * i2 + 5]));
+            float t3, t4;
+            const int c2 = ClosestHitBVH(r2.orig, r2.dir, bv, t3, stk, 1);
+            for (int li : {other, b}) {
+                if (li < 0) continue;
+                bool lit = true;
+                const int c3 = ClosestHitDualBVH4(r.orig, r2.dir, true, r.dir, li, sph[li], bv, t4, lit, stk, 1);
+                if (c3 != c2 || memcmp(&t3, &t4, 4) != 0 || lit != (b == li)) bad += 1;
+            }
+            bool lit = true;
+            const int c4 = ClosestHitDualBVH4(r.orig, r2.dir, false, r.dir, 0, sph[0], bv, t4, lit, stk, 1);
+            if (c4 != c2 || memcmp(&t3, &t4, 4) != 0 || lit) bad += 1;
+        }
         sn += st.nodes;
         ss += st.spheres;
         mn = std::max(mn, (double)st.nodes);
@@ -1862,10 +1976,11 @@ int lrt_scatter_eval(const lrt_sphere* spheres, const lrt_material* materials, i
     const unsigned blocks = (unsigned)((n + 63) / 64);
     if (bvh)
         scatter_probe_kernel<true><<<blocks, 64>>>(sc, (const int*)dd[6], (const float*)dd[7], (const float*)dd[8],
-                                                   (const uint32_t*)dd[9], n, o_out, o_ret, o_cnt, o_st);
+                                                   (const uint32_t*)dd[9], n, o_out, o_ret, o_cnt, o_st,
+                                                   on_device == 2);
     else
         scatter_probe_kernel<false><<<blocks, 64>>>(sc, (const int*)dd[6], (const float*)dd[7], (const float*)dd[8],
-                                                    (const uint32_t*)dd[9], n, o_out, o_ret, o_cnt, o_st);
+                                                    (const uint32_t*)dd[9], n, o_out, o_ret, o_cnt, o_st, 0);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e == hipSuccess) e = hipMemcpy(out, o_out, sizeof(float) * 12 * n, hipMemcpyDeviceToHost);
@@ -1874,6 +1989,64 @@ int lrt_scatter_eval(const lrt_sphere* spheres, const lrt_material* materials, i
     if (e == hipSuccess) e = hipMemcpy(state, o_st, sizeof(uint32_t) * n, hipMemcpyDeviceToHost);
     release();
     if (e != hipSuccess) return fail(LRT_E_HIP, std::string("scatter probe: ") + hipGetErrorString(e));
+    return LRT_OK;
+}
+
+int lrt_bvh_eval(const lrt_sphere* spheres, int count, const float* rays, int n, int* ids, float* ts, int mode) {
+    if (!spheres || count < 2 || !rays || !ids || !ts || n < 0 || mode < 0 || mode > 2)
+        return fail(LRT_E_INVALID, "bvh eval: invalid arguments");
+    std::vector<float4> sph(count);
+    for (int i = 0; i < count; ++i) {
+        const float r = spheres[i].radius;
+        sph[i] = make_float4(spheres[i].center.x, spheres[i].center.y, spheres[i].center.z, r * r);
+    }
+    BvhHost H;
+    build_bvh_host(spheres, count, sph, H);
+    BvhView bv;
+    bv.margin = H.margin;
+    bv.on = 1;
+    bv.nnodes = (int)(H.nodes.size() / (LRT_BVH4 ? 8 : 4));
+    bv.big0 = H.big0;
+    bv.nbig = H.nbig;
+    if (mode == 0) {
+        bv.nodes = H.nodes.data();
+        bv.lsph = H.lsph.data();
+        bv.lid = H.lid.data();
+        unsigned short stk[kBvhStackLevels];
+        for (int i = 0; i < n; ++i) {
+            const Ray r = make_ray(f3(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]),
+                                   f3(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]));
+            ids[i] = ClosestHitBVH(r.orig, r.dir, bv, ts[i], stk, 1);
+        }
+        return LRT_OK;
+    }
+    if (n == 0) return LRT_OK;
+    void *d_nodes = nullptr, *d_lsph = nullptr, *d_lid = nullptr, *d_rays = nullptr, *d_ids = nullptr, *d_ts = nullptr;
+    hipError_t e = hipMalloc(&d_nodes, sizeof(float4) * std::max<size_t>(H.nodes.size(), 8));
+    if (e == hipSuccess) e = hipMalloc(&d_lsph, sizeof(float4) * H.lsph.size());
+    if (e == hipSuccess) e = hipMalloc(&d_lid, sizeof(int) * H.lid.size());
+    if (e == hipSuccess) e = hipMalloc(&d_rays, sizeof(float) * 6 * (size_t)n);
+    if (e == hipSuccess) e = hipMalloc(&d_ids, sizeof(int) * (size_t)n);
+    if (e == hipSuccess) e = hipMalloc(&d_ts, sizeof(float) * (size_t)n);
+    if (e == hipSuccess && !H.nodes.empty())
+        e = hipMemcpy(d_nodes, H.nodes.data(), sizeof(float4) * H.nodes.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d_lsph, H.lsph.data(), sizeof(float4) * H.lsph.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d_lid, H.lid.data(), sizeof(int) * H.lid.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d_rays, rays, sizeof(float) * 6 * (size_t)n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        bv.nodes = (const float4*)d_nodes;
+        bv.lsph = (const float4*)d_lsph;
+        bv.lid = (const int*)d_lid;
+        bvh_probe_kernel<<<(unsigned)((n + 63) / 64), 64>>>(bv, (const float*)d_rays, n, (int*)d_ids, (float*)d_ts,
+                                                          mode == 2);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(ids, d_ids, sizeof(int) * (size_t)n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(ts, d_ts, sizeof(float) * (size_t)n, hipMemcpyDeviceToHost);
+    for (void* p : {d_nodes, d_lsph, d_lid, d_rays, d_ids, d_ts})
+        if (p) (void)hipFree(p);
+    if (e != hipSuccess) return fail(LRT_E_HIP, std::string("bvh eval: ") + hipGetErrorString(e));
     return LRT_OK;
 }
 

@@ -1,0 +1,299 @@
+// v5 (LRT_F_POOL): the v0 per-pixel loop with SAMPLE-POOL regeneration inside the wave.
+//
+// In v0 a wave task is a tile of pixels x frames, one pixel-sample per lane, and the bounce
+// loop runs until the task's longest path ends. At 1000 spheres the closest-hit and shadow
+// traversals dominate, and their wave executions carry few lanes: config 4 section counts
+// (LRT_EXP_SECSTATS, profiles/r2_sec1) show ~6.7 bounce iterations per wave task while a
+// path averages ~1.7 closest hits, so secondary closest-hit passes run at 20 lanes of 64
+// and shadow passes at 10.
+//
+// Here a wave owns a tile of kPix pixels and works through a POOL of its pixel-samples,
+// up to kPoolSamples per round (frame-major: sample k is frame fr0 + k / kPix of pixel
+// k % kPix). A lane whose path ends folds its recursion stack (Trace's return value,
+// parallel.cpp:214), stores the colour in the wave's slot k and takes the next sample
+// index at once (ballot + mbcnt: no atomics). Every bounce iteration therefore traces
+// (nearly) 64 paths until the pool runs dry. When the round's pool is done, lane j < kPix
+// applies TraceRowJob's progressive lerp (parallel.cpp:262,280-286) to pixel j's colours
+// in frame order -- the serial chain, so the result is bit-identical to the reference's
+// frame-by-frame loop -- and the next round (or tile) starts.
+//
+// Same per-ray arithmetic, RNG streams (PixelSeed(x, y, f)), draw order, ray counting,
+// Scatter and recursion fold as Trace (lrt_trace.h). The colour slots live in global
+// memory (16 KB per resident wave, L2-resident): LDS already holds the recursion stack.
+#pragma once
+
+namespace lrt {
+
+constexpr int kPoolSamples = 1024;   // colour slots per wave: samples per round of a tile
+enum : int { kPoolIdle = 0, kPoolTrace = 1, kPoolDone = 2 };
+
+template <int kPix>
+struct PoolTile {   // tile shape: kPix pixels, as square as a power of two allows
+    static constexpr int X = kPix >= 64 ? 8 : kPix >= 16 ? 4 : kPix >= 4 ? 2 : 1;
+    static constexpr int Y = kPix / X;
+    static_assert(X * Y == kPix && kPix <= 64, "kPix: 1, 4, 16 or 64");
+};
+
+template <int MAXD, bool kLds, bool kBvh, int kPix, int kNS = 0>
+__global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const KernelArgs a) {
+    static_assert(kNS == 0 || (kLds && !kBvh), "a fixed sphere count is for the LDS linear scan");
+    // LDS as trace_kernel: [recursion stack kTraceLdsLevels x 64][powf tables][renormalize
+    // table unless kBvh][spheres][materials][lights][bvh stack at a.bvh_stack_offset]
+    extern __shared__ float4 smem[];
+    const int lane = threadIdx.x;
+    double* s_pow = reinterpret_cast<double*>(smem + kTraceLdsLevels * 64);
+    {
+        const libm::PowTables g = libm::pow_tables();
+        for (int i = lane; i < 16; i += 64) {
+            s_pow[i] = g.invc[i];
+            s_pow[16 + i] = g.logc[i];
+        }
+        for (int i = lane; i < 32; i += 64) reinterpret_cast<uint64_t*>(s_pow + 32)[i] = g.exp2[i];
+    }
+    constexpr int kLutBytes = kBvh ? 0 : kRenormBytes;
+    float* s_lut = kBvh ? nullptr : reinterpret_cast<float*>(s_pow + 64);
+    if (!kBvh) renorm_lut_fill(s_lut, lane, 64);
+    float4* s_sph = smem + kTraceLdsLevels * 64 + (kPowTableBytes + kLutBytes) / 16;
+    float4* s_mat = s_sph + a.count;
+    int* s_lights = reinterpret_cast<int*>(s_mat + 3 * a.count);
+    if (kLds) {
+        for (int i = lane; i < a.count; i += 64) s_sph[i] = a.sph[i];
+        for (int i = lane; i < 3 * a.count; i += 64) s_mat[i] = a.mats[i];
+        for (int i = lane; i < a.nlights; i += 64) s_lights[i] = a.lights[i];
+    }
+    __syncthreads();
+    SceneView sc;
+    sc.pow.invc = s_pow;
+    sc.pow.logc = s_pow + 16;
+    sc.pow.exp2 = reinterpret_cast<const uint64_t*>(s_pow + 32);
+    sc.rnlut = s_lut;
+    sc.sph = kLds ? s_sph : a.sph;
+    sc.gsph = a.sph;
+    sc.mats = kLds ? s_mat : a.mats;
+    sc.lights = kLds ? s_lights : a.lights;
+    sc.count = a.count;
+    sc.nlights = a.nlights;
+    sc.bv = a.bv;
+    sc.bstk = reinterpret_cast<unsigned short*>(reinterpret_cast<char*>(smem) + a.bvh_stack_offset) + lane;
+    sc.bstride = 64;
+#ifdef LRT_EXP_SECSTATS
+    __shared__ unsigned long long s_sectime[2 + 3 * kSecN];
+    sc.secstats = a.wtrace;
+    sc.sectime = s_sectime;
+    if (lane == 0) {
+        for (int k = 0; k < 2 + 3 * kSecN; ++k) sc.sectime[k] = 0;
+        sc.sectime[0] = kSecOther;
+        sc.sectime[1] = __builtin_amdgcn_s_memtime();
+    }
+#endif
+    float4* const lstk = smem + lane;   // this lane's recursion stack (LDS)
+    const size_t gtid = (size_t)blockIdx.x * 64 + lane;
+    const size_t gthreads = (size_t)gridDim.x * 64;
+    float4* const gstk = a.ovf + gtid;   // levels >= kTraceLdsLevels (MAXD > 8)
+    auto put = [&](int lvl, float4 v) {
+        if (MAXD <= kTraceLdsLevels || lvl < kTraceLdsLevels) lstk[lvl * 64] = v;
+        else gstk[(size_t)(lvl - kTraceLdsLevels) * gthreads] = v;
+    };
+    auto get = [&](int lvl) -> float4 {
+        if (MAXD <= kTraceLdsLevels || lvl < kTraceLdsLevels) return lstk[lvl * 64];
+        return gstk[(size_t)(lvl - kTraceLdsLevels) * gthreads];
+    };
+    float4* const slots = a.colbuf + (size_t)blockIdx.x * kPoolSamples;
+
+    constexpr int TX = PoolTile<kPix>::X, TY = PoolTile<kPix>::Y;
+    constexpr int kRoundFrames = kPoolSamples / kPix;
+    const int tilesX = (a.xc + TX - 1) / TX;
+    const int ntiles = tilesX * ((a.rows + TY - 1) / TY);
+    const float invWidth = 1.0f / (float)a.width;     // parallel.cpp:260
+    const float invHeight = 1.0f / (float)a.height;   // parallel.cpp:261
+    const int fend = a.frame0 + a.frames;
+    const unsigned long long below = (1ull << lane) - 1ull;   // lanes before this one
+    int rays = 0;
+    // tile queues, as v0: block b serves queue b % kV0Queues (XCD-local counters)
+    const int q = blockIdx.x % kV0Queues;
+    const int bq = ((int)gridDim.x - q + kV0Queues - 1) / kV0Queues;
+    const int nq = (ntiles - q + kV0Queues - 1) / kV0Queues;
+    unsigned long long* ctr = a.tiles + q * kCtrStride;
+    for (int i = blockIdx.x / kV0Queues; i < nq;) {
+        const int tile = q + kV0Queues * i;
+        const int tx0 = (tile % tilesX) * TX, ty0 = (tile / tilesX) * TY;
+        unsigned long long fetched = 0;
+        if (lane == 0) fetched = atomicAdd(ctr, 1ull);   // consumed after the tile (hides its latency)
+        // lane j < kPix owns pixel j of the tile for the lerp chain and the store
+        const int mx = tx0 + lane % TX, my = ty0 + (lane / TX) % TY;
+        const bool mine = lane < kPix && mx < a.xc && my < a.rows;
+        float4* const mpx = a.out + (size_t)my * a.xc + mx;
+        float4 acc = mine ? *mpx : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        for (int fr0 = a.frame0; fr0 < fend; fr0 += kRoundFrames) {
+            const int nfr = fend - fr0 < kRoundFrames ? fend - fr0 : kRoundFrames;
+            const int N = nfr * kPix;   // this round's pool
+            int next = 0, state = kPoolIdle, k = 0, depth = 0;
+            bool prevLambert = false;
+            uint32_t rng = 1;
+            Ray r;   // the ray to trace next (a camera ray, or the last scatter's bounce ray)
+            r.orig = f3(0.0f, 0.0f, 0.0f);
+            r.dir = f3(0.0f, 1.0f, 0.0f);
+            // the last scatter event, pushed on the stack but not yet counted in `depth`: its
+            // deferred shadow ray (the last light's, as TraceDual) is traced in the same
+            // pass as the bounce ray; carry = its stack value should the light be reached
+            bool pend = false;
+            F3 carry = f3(0.0f, 0.0f, 0.0f);
+            DeferredLight dl;
+            dl.on = false;
+            dl.li = -1;
+            dl.l = f3(0.0f, 0.0f, 0.0f);
+            dl.contrib = f3(0.0f, 0.0f, 0.0f);
+            for (;;) {
+                // ---- refill: lanes without a path take the pool's next samples --------------
+                const unsigned long long needM = __ballot(state == kPoolIdle);
+                if (needM) {
+                    if (state == kPoolIdle) {
+                        k = next + __popcll(needM & below);
+                        state = kPoolDone;
+                        if (k < N) {
+                            const int j = k % kPix, f = fr0 + k / kPix;
+                            const int lx = tx0 + j % TX, ly = ty0 + j / TX;
+                            if (lx < a.xc && ly < a.rows) {   // TraceRowJob's per-pixel body (:270-279)
+                                sec_count(sc, kSecCamera);
+                                const int x = a.x0 + lx;
+                                const int y = a.y0 + (ly / a.rb) * a.rb * a.rp + a.rph * a.rb + ly % a.rb;
+                                rng = PixelSeed((uint32_t)x, (uint32_t)y, (uint32_t)f);
+                                const float u = ((float)x + RandomFloat01(rng)) * invWidth;    // :272
+                                const float v = ((float)y + RandomFloat01(rng)) * invHeight;   // :273
+                                r = GetRay(a.cam, u, v, rng, sc.rnlut);
+                                depth = 0;
+                                prevLambert = false;
+                                pend = false;
+                                state = kPoolTrace;
+                            } else {
+                                state = kPoolIdle;   // outside the window: nothing to trace
+                            }
+                        }
+                    }
+                    next += __popcll(needM);
+                }
+                const unsigned long long traceM = __ballot(state == kPoolTrace);
+                if (traceM == 0) {
+                    if (__ballot(state == kPoolIdle) == 0) break;   // the pool is dry: round done
+                    continue;
+                }
+                // camera rays that all start together (a round's first iteration) take the
+                // packet traversal (lrt_bvh.h)
+                const bool coherent = kBvh && LRT_PACKET_DEPTH > 0 && __ballot(state == kPoolTrace && depth != 0) == 0 &&
+                                      __ballot(state == kPoolTrace && pend) == 0;
+                sec_enter(sc, kSecOther, false);
+                // ---- one bounce of every traced path: Trace's body (parallel.cpp:202-226) ----
+                if (state == kPoolTrace) {
+                    // HitWorld of r (:204-205) and the pending shadow ray (:122-123) in one pass
+                    sec_count(sc, coherent ? kSecHit0 : kSecHit);
+                    ++rays;
+                    int nid;
+                    float nt;
+                    bool lit = false;
+                    const bool hasS = pend && dl.on;
+                    if constexpr (kBvh) {
+                        if (coherent) {
+                            nid = ClosestHitBVH(r.orig, r.dir, sc.bv, nt, sc.bstk, sc.bstride, nullptr, true);
+                        } else {
+                            const float4 ls = hasS ? sc.sph[dl.li] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                            nid = ClosestHitDualBVH4(r.orig, r.dir, hasS, dl.l, dl.li, ls, sc.bv, nt, lit, sc.bstk,
+                                                     sc.bstride);
+                        }
+                    } else {
+                        int sid;
+                        DualClosestHit<kNS>(r.orig, r.dir, hasS, dl.l, sc, nid, nt, sid);
+                        lit = hasS && sid == dl.li;
+                    }
+                    if (pend) {   // the scatter event that produced r (:214), with its light if reached
+                        if (lit) put(depth, make_float4(carry.x, carry.y, carry.z, __int_as_float(dl.id)));
+                        ++depth;
+                        pend = false;
+                    }
+                    F3 leaf;
+                    bool fin = false;
+                    if (nid < 0) {   // sky (:223-225)
+                        const float t = 0.5f * (r.dir.y + 1.0f);
+                        leaf = ((1.0f - t) * f3(1.0f, 1.0f, 1.0f) + t * f3(0.5f, 0.7f, 1.0f)) * 0.3f;
+                        fin = true;
+                    } else {   // HitWorld's winner (maths.cpp:74-76,86-88), then Scatter (:210-212)
+                        const float4 sp4 = sc.sph[nid];
+                        Hit rec;
+                        rec.pos = point_at(r, nt);
+                        rec.normal = normalize(rec.pos - f3(sp4.x, sp4.y, sp4.z));
+                        rec.t = nt;
+                        const Material mat = load_material(sc.mats, nid);
+                        F3 matE = mat.emissive;
+                        fin = true;
+                        leaf = matE;
+                        if (depth < a.maxDepth) {
+                            F3 lightE;
+                            dl.on = false;
+                            const F3 X = ScatterDir<kBvh, kNS>(mat, nid, r, rec, lightE, rays, rng, sc, &dl, coherent);
+                            sec_count(sc, kSecPost);
+                            const F3 dir = renormalize(normalize(X), sc.rnlut);   // Ray(rec.pos, normalize(X))
+                            if (mat.type != 1 || dot(dir, rec.normal) > 0.0f) {    // Metal absorbs (:147)
+                                if (a.ndl && prevLambert) matE = f3(0.0f, 0.0f, 0.0f);
+                                prevLambert = mat.type == 0;
+                                const F3 e = matE + lightE;
+                                put(depth, make_float4(e.x, e.y, e.z, __int_as_float(nid)));
+                                if (dl.on) carry = matE + (lightE + dl.contrib);   // TraceDual's order
+                                dl.id = nid;
+                                pend = true;
+                                r.orig = rec.pos;
+                                r.dir = dir;
+                                fin = false;
+                            }
+                        }
+                    }
+                    if (fin) {   // :214 folded leaf-outwards; the colour goes to the sample's slot
+                        sec_count(sc, kSecFold);
+                        F3 T = leaf;
+                        for (int d = depth - 1; d >= 0; --d) {
+                            const float4 s = get(d);
+                            const float4 b = sc.mats[3 * __float_as_int(s.w) + 2];
+                            T = f3(s.x, s.y, s.z) + f3(b.x, b.y, b.z) * T;
+                        }
+                        slots[k] = make_float4(T.x, T.y, T.z, 0.0f);
+                        state = kPoolIdle;
+                    }
+                }
+            }
+            // ---- the round's colours in frame order, one lane per pixel (:262,282) ---------
+            sec_enter(sc, kSecOther, false);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (mine) {
+                F3 c3 = f3(acc.x, acc.y, acc.z);
+                for (int t = 0; t < nfr; ++t) {
+                    const float4 c = slots[t * kPix + lane];
+                    const int f = fr0 + t;
+                    const float lerpFac = f < kLerpTable ? a.lerp[f] : (float)f / (float)(f + 1);
+                    c3 = c3 * lerpFac + f3(c.x, c.y, c.z) * (1.0f - lerpFac);
+                }
+                acc.x = c3.x;
+                acc.y = c3.y;
+                acc.z = c3.z;
+            }
+            // the next round overwrites the slots: every read above completes first
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
+        if (mine) *mpx = acc;   // alpha as read
+        const unsigned long long n = __shfl(fetched, 0, 64) + (unsigned long long)bq;
+        i = n < (unsigned long long)nq ? (int)n : nq;
+    }
+#ifdef LRT_EXP_SECSTATS
+    sec_enter(sc, kSecOther, false);
+    if (lane == 0)
+        for (int k = 0; k < kSecN; ++k) {
+            unsigned long long* g = sc.secstats + 3 * (k + kSecN * (blockIdx.x & 15));
+            atomicAdd(g, sc.sectime[2 + kSecN + k]);
+            atomicAdd(g + 1, sc.sectime[2 + 2 * kSecN + k]);
+            atomicAdd(g + 2, sc.sectime[2 + k]);
+        }
+#endif
+    const unsigned long long total = wave_sum((unsigned long long)rays);
+    if (lane == 0) block_epilogue(a.tiles, a.rays, q, bq, total);
+}
+
+}  // namespace lrt

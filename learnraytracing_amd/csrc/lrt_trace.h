@@ -243,7 +243,8 @@ struct SceneView {
 // it, how many lanes are active then, and the shader cycles spent in it until the next
 // section switch (s_memtime, bookkept in LDS by the first active lane so divergence
 // cannot desynchronise it). sec_count enters and counts; sec_enter only switches time.
-enum { kSecHit, kSecLambert, kSecShadow, kSecMetal, kSecDiel, kSecPost, kSecFold, kSecCamera, kSecOther, kSecN };
+enum { kSecHit, kSecLambert, kSecShadow, kSecMetal, kSecDiel, kSecPost, kSecFold, kSecCamera, kSecOther, kSecHit0,
+       kSecShadow0, kSecN };   // *0: a path's first closest hit / first shadow rays (coherent)
 LRT_DEV void sec_enter(const SceneView& sc, int sec, bool count) {
 #if defined(LRT_EXP_SECSTATS) && defined(__HIP_DEVICE_COMPILE__)
     const unsigned long long m = __ballot(1);
@@ -312,8 +313,10 @@ LRT_DEV void SphereRoots(float rsProj, float ifHit, float tMin, float& closestT,
 // kNS > 0: the scene has exactly kNS spheres (the reference's kSphereCount is a compile-time
 // 9, parallel.cpp:27): the scan is fully unrolled with constant LDS offsets.
 template <bool kBvh = false, int kNS = 0>
-LRT_DEV int ClosestHitSV(const Ray& r, float tMin, float tMax, const SceneView& sc, float& tOut) {
-    if (kBvh) return ClosestHitBVH(r.orig, r.dir, sc.bv, tOut, sc.bstk, sc.bstride);   // tMin/tMax = kMinT/kMaxT
+LRT_DEV int ClosestHitSV(const Ray& r, float tMin, float tMax, const SceneView& sc, float& tOut,
+                         bool coherent = false) {
+    if (kBvh)   // tMin/tMax = kMinT/kMaxT
+        return ClosestHitBVH(r.orig, r.dir, sc.bv, tOut, sc.bstk, sc.bstride, nullptr, coherent);
     float closestT = tMax;
     int id = -1;
     const ConstFPtr csph = (ConstFPtr)sc.gsph;
@@ -355,10 +358,11 @@ LRT_DEV int ClosestHit(const F3& o, const F3& d, const float4* sph, int count, f
 }
 
 template <bool kBvh = false, int kNS = 0>
-LRT_DEV bool HitWorld(const Ray& r, float tMin, float tMax, const SceneView& sc, Hit& outHit, int& outID) {
+LRT_DEV bool HitWorld(const Ray& r, float tMin, float tMax, const SceneView& sc, Hit& outHit, int& outID,
+                      bool coherent = false) {
     float closestT;
-    sec_count(sc, kSecHit);
-    const int id = ClosestHitSV<kBvh, kNS>(r, tMin, tMax, sc, closestT);
+    sec_count(sc, coherent ? kSecHit0 : kSecHit);
+    const int id = ClosestHitSV<kBvh, kNS>(r, tMin, tMax, sc, closestT, coherent);
     if (id < 0) return false;
     float4 s = sc.sph[id];
     outHit.pos = point_at(r, closestT);
@@ -384,11 +388,13 @@ struct DeferredLight {
     F3 l, contrib;   // l: the shadow ray's direction
     int li;
     bool on;
+    int id;          // the scattering sphere (pool kernel: its stack entry's material)
 };
 
 template <bool kBvh = false, int kNS = 0>
 LRT_DEV F3 ScatterDir(const Material& mat, int matId, const Ray& r_in, const Hit& rec, F3& outLightE,
-                      int& inoutRayCount, uint32_t& rng, const SceneView& sc, DeferredLight* defer = nullptr) {
+                      int& inoutRayCount, uint32_t& rng, const SceneView& sc, DeferredLight* defer = nullptr,
+                      bool coherent = false) {
     outLightE = f3(0.0f, 0.0f, 0.0f);
     if (mat.type == 0) {  // Lambert :81-136
         sec_count(sc, kSecLambert);
@@ -432,13 +438,13 @@ LRT_DEV F3 ScatterDir(const Material& mat, int matId, const Ray& r_in, const Hit
                 defer->on = true;
                 continue;
             }
-            sec_count(sc, kSecShadow);
+            sec_count(sc, coherent ? kSecShadow0 : kSecShadow);
             bool lit;
             if constexpr (kBvh) {
                 Ray sr;
                 sr.orig = rec.pos;
                 sr.dir = renormalize(l, sc.rnlut);
-                lit = ShadowReachesLightBVH(sr.orig, sr.dir, i, s, sc.bv, sc.bstk, sc.bstride);
+                lit = ShadowReachesLightBVH(sr.orig, sr.dir, i, s, sc.bv, sc.bstk, sc.bstride, coherent);
             } else {
                 Ray sr;
                 sr.orig = rec.pos;
@@ -493,11 +499,12 @@ LRT_DEV F3 ScatterDir(const Material& mat, int matId, const Ray& r_in, const Hit
 // reference absorbs (Metal scattered below the surface, :147). The RNG state and the scene
 // are explicit parameters, as in the reference's own per-stream variant
 // (src/cpu/README.md:42, fragmentShader.fs.glsl:175-218). `mat.id` is the material's table
-// index, the reference's `&mat` identity.
+// index, the reference's `&mat` identity. coherent: the active lanes' shadow rays start
+// together (packet traversal, lrt_bvh.h).
 template <bool kBvh = false, int kNS = 0>
 LRT_DEV bool Scatter(const Material& mat, const Ray& r_in, const Hit& rec, F3& attenuation, Ray& scattered,
-                     F3& outLightE, int& inoutRayCount, uint32_t& rng, const SceneView& sc) {
-    const F3 X = ScatterDir<kBvh, kNS>(mat, mat.id, r_in, rec, outLightE, inoutRayCount, rng, sc);
+                     F3& outLightE, int& inoutRayCount, uint32_t& rng, const SceneView& sc, bool coherent = false) {
+    const F3 X = ScatterDir<kBvh, kNS>(mat, mat.id, r_in, rec, outLightE, inoutRayCount, rng, sc, nullptr, coherent);
     scattered.orig = rec.pos;
     scattered.dir = renormalize(normalize(X), sc.rnlut);   // Ray(rec.pos, normalize(X))
     attenuation = mat.att;                                  // albedo, or (1, 1, 1) for Dielectric (:192)
@@ -546,7 +553,9 @@ LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const S
         Hit rec;
         int id = 0;
         ++inoutRayCount;
-        if (!HitWorld<kBvh, kNS>(r, kMinT, kMaxT, sc, rec, id)) {
+        // the first rays of a wave's paths start together: packet traversal (lrt_bvh.h)
+        const bool coherent = depth < LRT_PACKET_DEPTH;
+        if (!HitWorld<kBvh, kNS>(r, kMinT, kMaxT, sc, rec, id, coherent)) {
             float t = 0.5f * (r.dir.y + 1.0f);
             leaf = ((1.0f - t) * f3(1.0f, 1.0f, 1.0f) + t * f3(0.5f, 0.7f, 1.0f)) * 0.3f;
             break;
@@ -561,7 +570,8 @@ LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const S
         F3 lightE, attenuation;
         Ray scattered;
         // :212 -- the attenuation is the material's `att` row, which the fold reads back by id
-        if (depth < maxDepth && Scatter<kBvh, kNS>(mat, r, rec, attenuation, scattered, lightE, inoutRayCount, rng, sc)) {
+        if (depth < maxDepth &&
+            Scatter<kBvh, kNS>(mat, r, rec, attenuation, scattered, lightE, inoutRayCount, rng, sc, coherent)) {
             sec_count(sc, kSecPost);
             if (ndl && prevLambert) matE = f3(0.0f, 0.0f, 0.0f);
             prevLambert = mat.type == 0;

@@ -20,6 +20,8 @@ from learnraytracing_amd import _lib as L
 pytestmark = pytest.mark.gpu
 
 NO_BVH = 32
+V0, POOL = 2, 512   # LRT_F_SIMPLE (trace_kernel), LRT_F_POOL (pool_kernel)
+KERNELS = pytest.mark.parametrize("kflags", [V0, POOL], ids=["v0", "pool"])
 
 
 def _bitwise(got, want, what):
@@ -48,57 +50,66 @@ def _render(gpu, flags=0, **kw):
     return buf, rays, L.last_launch()
 
 
-def _assert_instance(info, split, samp="0"):
-    assert info["kernel"] == "trace_kernel" and info["bvh"] == "1" and info["maxd"] == "8", info
-    assert info["split"] == str(split) and info["samp"] == samp, info
+def _assert_instance(info, kflags, frames, samp="0"):
+    """The instance the benchmark runs for this geometry: trace_kernel with 16 frame lanes
+    per pixel (v0), or pool_kernel with its tile size for `frames`."""
+    assert info["bvh"] == "1" and info["maxd"] == "8", info
+    if kflags == POOL:
+        assert info["kernel"] == "pool_kernel" and info["pix"] == str(16 if frames <= 64 else 4), info
+    else:
+        assert info["kernel"] == "trace_kernel" and info["split"] == "16" and info["samp"] == samp, info
 
 
+@KERNELS
 @pytest.mark.parametrize("name", ["scene1000_c4_s64", "scene1000_c5_s256"])
-def test_config_instance_vs_reference_golden(gpu, scene1000, manifest, images, name):
+def test_config_instance_vs_reference_golden(gpu, scene1000, manifest, images, name, kflags):
     """64 / 256 spp windows of configs 4 / 5 equal the reference's own render."""
     fx = manifest["fixtures"][name]
     assert fx["source"].startswith("reference")
-    buf, rays, info = _render(gpu, width=fx["w"], height=fx["h"], frames=fx["frames"], max_depth=fx["max_depth"],
-                              x0=fx["x0"], x_count=fx["xc"], y0=fx["y0"], row_count=fx["yc"])
-    _assert_instance(info, 16)
+    buf, rays, info = _render(gpu, flags=kflags, width=fx["w"], height=fx["h"], frames=fx["frames"],
+                              max_depth=fx["max_depth"], x0=fx["x0"], x_count=fx["xc"], y0=fx["y0"], row_count=fx["yc"])
+    _assert_instance(info, kflags, fx["frames"])
     _bitwise(buf, images[name], name)
     assert rays == fx["rays"]
 
 
-def test_config4_window_vs_oracle_and_linear_scan(gpu, scene1000):
+@KERNELS
+def test_config4_window_vs_oracle_and_linear_scan(gpu, scene1000, kflags):
     """A 64x24 window of config 4 at 64 spp: BVH == C restatement == GPU linear scan."""
     s, m = scene1000
     kw = dict(width=3840, height=2160, frames=64, max_depth=8, x0=1880, x_count=64, y0=1000, row_count=24)
-    a, ra, info = _render(gpu, **kw)
-    _assert_instance(info, 16)
+    a, ra, info = _render(gpu, flags=kflags, **kw)
+    _assert_instance(info, kflags, 64)
     want, wr = oracle.orc_render(3840, 2160, 64, 8, 0, 1880, 64, 1000, 24, spheres=s, mats=m, threads=16)
     _bitwise(a, want, "config4 window vs oracle")
     assert ra == wr
-    b, rb, info_b = _render(gpu, flags=NO_BVH, **kw)
-    assert info_b["bvh"] == "0" and info_b["split"] == "16"
+    b, rb, info_b = _render(gpu, flags=NO_BVH | kflags, **kw)
+    assert info_b["bvh"] == "0" and info_b["kernel"] == info["kernel"]
     assert rb == ra and np.array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
-def test_config4_many_tiles_bvh_equals_linear_scan(gpu, scene1000):
+@KERNELS
+def test_config4_many_tiles_bvh_equals_linear_scan(gpu, scene1000, kflags):
     """Enough 64-spp tiles that the persistent grid refills from its queues several times
     (every block runs many tasks): BVH == linear scan, rays included."""
     kw = dict(width=3840, height=2160, frames=64, max_depth=8, x0=1536, x_count=768, y0=900, row_count=96)
-    a, ra, info = _render(gpu, **kw)
-    _assert_instance(info, 16)
+    a, ra, info = _render(gpu, flags=kflags, **kw)
+    _assert_instance(info, kflags, 64)
     assert int(info["tasks"]) > int(info["grid"])
-    b, rb, _ = _render(gpu, flags=NO_BVH, **kw)
+    b, rb, _ = _render(gpu, flags=NO_BVH | kflags, **kw)
     assert rb == ra and np.array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
-def test_config5_shard_of_8_vs_oracle(gpu, scene1000):
+@KERNELS
+def test_config5_shard_of_8_vs_oracle(gpu, scene1000, kflags):
     """Rank 3's row-block-cyclic shard of an 8-GPU config-5 frame (row blocks of 8, 256 spp
     per pixel -- the strong-scaling shape, BVH without sample mode): two row bands of a
     24-column window against the restatement."""
     s, m = scene1000
     W, H, rb, G, ph, y0 = 7680, 4320, 8, 8, 3, 2048
-    a, ra, info = _render(gpu, width=W, height=H, frames=256, max_depth=8, x0=3800, x_count=24, y0=y0,
+    a, ra, info = _render(gpu, flags=kflags, width=W, height=H, frames=256, max_depth=8, x0=3800, x_count=24, y0=y0,
                           row_count=16, row_block=rb, row_period=G, row_phase=ph)
-    _assert_instance(info, 16)
+    _assert_instance(info, kflags, 256)
     rays = 0
     for band in range(2):   # local rows 8*band.. map to y0 + band*rb*G + ph*rb ..
         gy = y0 + band * rb * G + ph * rb

@@ -41,7 +41,7 @@ def test_golden_mode_p(gpu, manifest, images, name):
     assert rays == fx["rays"]
 
 
-@pytest.mark.parametrize("flags", [0, 1, 2, 3, 128, 129, 256, 257])
+@pytest.mark.parametrize("flags", [0, 1, 2, 3, 128, 129, 256, 257, 512, 513])
 @pytest.mark.parametrize("name", ["p_160x90_s4_d8", "p_96x54_s1_d50"])
 def test_golden_kernel_variants(gpu, manifest, images, flags, name):
     """Every kernel (v0 default / LRT_F_SIMPLE, v3 LRT_F_V3, v4 LRT_F_WAVEFRONT), with
@@ -294,7 +294,7 @@ def test_deterministic_repeat_full_config2(gpu):
 
 
 @pytest.mark.parametrize("n,seed", [(17, 3), (200, 5), (1000, 1), (4096, 7)])
-@pytest.mark.parametrize("kflags", [2, 128, 256])
+@pytest.mark.parametrize("kflags", [2, 128, 256, 512])
 def test_bvh_equals_linear_scan(gpu, n, seed, kflags):
     """The BVH closest hit returns the reference's scan result bit for bit: same
     pixels and ray counts as LRT_F_NO_BVH, for every kernel."""
@@ -371,7 +371,8 @@ def test_cu_reserved_render_stream(gpu):
 
 V3 = 128   # LRT_F_V3: path regeneration inside the wave
 WF = 256   # LRT_F_WAVEFRONT: breadth-first kernels over compacted queues
-ALT = pytest.mark.parametrize("kflags", [V3, WF], ids=["v3", "wavefront"])
+POOL = 512   # LRT_F_POOL: sample-pool regeneration inside the wave
+ALT = pytest.mark.parametrize("kflags", [V3, WF, POOL], ids=["v3", "wavefront", "pool"])
 
 
 @ALT
@@ -481,7 +482,7 @@ EDGE_CASES = {
 }
 
 
-@pytest.mark.parametrize("kflags", [0, V3, WF], ids=["auto", "v3", "wavefront"])
+@pytest.mark.parametrize("kflags", [0, V3, WF, POOL], ids=["auto", "v3", "wavefront", "pool"])
 @pytest.mark.parametrize("case", list(EDGE_CASES), ids=list(EDGE_CASES))
 def test_edge_cases_vs_oracle(gpu, case, kflags):
     """Degenerate sizes, depth budgets 0/1/64, frame numbers at the lerp table's end and

@@ -145,6 +145,9 @@ def test_scatter_host_matches_reference(scene):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", [1, 2], ids=["per_lane", "packet"])
 @pytest.mark.parametrize("scene", list(scenes()), ids=lambda t: t[0])
-def test_scatter_device_matches_reference(gpu, scene):
-    check_scene(*scene, on_device=1)
+def test_scatter_device_matches_reference(gpu, scene, mode):
+    """mode 2 sends every wave's shadow rays (64 unrelated cases) through the packet
+    traversal: exact whatever the rays' coherence."""
+    check_scene(*scene, on_device=mode)

@@ -10,6 +10,8 @@
 #   trace=C[,ARGS]    rocprofv3 --kernel-trace --stats of bench.py --config C --streams 1
 #   pmc=C,GROUP       one rocprofv3 --pmc pass (GROUP: fetch | write | sq | sq2) of bench --config C
 #   py=SCRIPT[,ARGS]  python SCRIPT ARGS (diagnostics under tools/)
+#   ab=V,C[,ARGS]     bench.py --config C with LRT_LIB=build_exp/liblrt_V.so (tools/build_variant.sh),
+#                     timed region only (A/B of library variants; V=default: the in-tree library)
 # Output: gpurun_out/$TAG/<step>.log (+ rocprof CSVs).
 cd "$GRAFT_REPO_ROOT" || exit 1
 TAG=${TAG:-latest}
@@ -58,6 +60,13 @@ for s in "$@"; do
            run "pmc_c${c}_$g" 300 rocprofv3 --pmc ${PMC[$g]} -d "$out" -o "pmc_c${c}_$g" --output-format csv -- \
              python3 bench.py --config "$c" --steps 2 --warmup 1 --streams 1 --no-cpu-baseline --no-extra-legs ;;
     py)    run "py$i" 600 python ${val//,/ } ;;
+    ab)    c2=${rest%%,*}
+           extra2=""
+           [[ "$rest" == *,* ]] && extra2=${rest#*,}
+           lib=build_exp/liblrt_$c.so
+           [ "$c" = default ] && lib=learnraytracing_amd/liblrt_hip.so
+           TAILN=1 run "ab_${c}_c${c2}_$i" 600 env LRT_LIB="$lib" python bench.py --config "$c2" --steps "$BSTEPS" \
+             --no-cpu-baseline --no-extra-legs ${extra2//;/ } ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
