@@ -355,7 +355,10 @@ def main():
         pix_samples = rows * W * spp_total                     # one launch on rank 0
         alg_bytes = BYTES_PER_PIXEL_SAMPLE * pix_samples
         key = f"{cfg_name}_n{shards}" if args.scaling == "strong" or shards == 1 else f"{cfg_name}_n{shards}_weak"
-        pmc = read_pmc(key) if not (args.spp or args.depth is not None or args.kernel not in ("auto", "v0")) else None
+        pmc = read_pmc(key) if not (args.spp or args.depth is not None or args.kernel != "auto") else None
+        if pmc and pmc.get("kernel") != launch_info.get("kernel"):
+            pmc = None   # counters of another kernel than this run's
+        kname = launch_info.get("kernel", "trace_kernel")
         dur_ms = alone_ms if alone_ms else ms_step
         hbm = {"bound": "hbm", "achieved": round(alg_bytes / (dur_ms * 1e-3) / 1e9, 3), "peak": HBM_PEAK_GBS,
                "unit": "GB/s", "frac": round(alg_bytes / (dur_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
@@ -370,7 +373,7 @@ def main():
             achieved_t = lane_ops / (dur_ms * 1e-3) / 1e12
             roof = {"bound": "valu", "achieved": round(achieved_t, 3), "peak": round(VALU_LANE_PEAK_T, 2),
                     "unit": "TFLOP/s", "frac": round(achieved_t / VALU_LANE_PEAK_T, 4),
-                    "traffic": hbm["traffic"], "kernel": "trace_kernel",
+                    "traffic": hbm["traffic"], "kernel": kname,
                     "lane_ops_per_launch": lane_ops,
                     "issue_frac": round(pmc["valu_insts_per_launch"] / (dur_ms * 1e-3) / VALU_ISSUE_PEAK, 4),
                     "lane_util": pmc["lane_util"],

@@ -500,107 +500,153 @@ LRT_DEV bool ShadowReachesLightBVH4(const F3& o, const F3& d, int li, const floa
 // light, `HitWorld(shadow ray) && hitID == li` is false (parallel.cpp:122-123), and the
 // query ends there. Same per-sphere arithmetic, conservative culling and (cand, index)
 // order as ClosestHitBVH4 / ShadowReachesLightBVH4, so both answers are bit-identical.
-LRT_DEV int ClosestHitDualBVH4(const F3& o, const F3& db, bool hasS, const F3& ds, int li, const float4& lightSph,
-                               const BvhView& bv, float& tOut, bool& lit, unsigned short* stk, int stride) {
-    float candL = kMaxT;
-    if (hasS) candL = SphereCand(o, ds, lightSph);
-    bool sh = candL < kMaxT;   // a light that is not hit at all is not lit (closestT starts at kMaxT)
-    lit = false;
-    F3 d = sh ? ds : db;
-    SlabRay sr = MakeSlabRay(o, d, bv.margin);
-    float bestT = sh ? candL : kMaxT;
-    int best = sh ? -2 : -1;   // position in lsph; -2: the light (index li); -1: nothing yet
-    auto test = [&](int pos, const float4& s) {
-        const F3 rs = f3(s.x, s.y, s.z) - o;                       // maths.cpp:54-59
-        const float rsProj = dot(rs, d);
-        const float ifHit = dot(rs, rs) - rsProj * rsProj - s.w;
-        if (ifHit < 0.0f) {
-            const float halfCut = sqrt_rn(-ifHit);
-            const float t1 = rsProj - halfCut;
-            const float t2 = rsProj + halfCut;
-            const float cand = t1 > kMinT ? t1 : (t2 > kMinT ? t2 : __builtin_inff());
-            if (cand < bestT ||
-                (cand == bestT && best != -1 && bv.lid[pos] < (best >= 0 ? bv.lid[best] : li))) {
-                bestT = cand;
-                best = pos;
-            }
-        }
-    };
-    for (int j = 0; j < bv.nbig; ++j) test(bv.big0 + j, bv.lsph[bv.big0 + j]);
-    int sp = 0, cur = 0, msk = bv.nnodes == 0 ? 0 : 0xF;
-    for (;;) {
-        bool qdone = msk == 0 || (sh && best != -2);   // stack exhausted, or the light is beaten
-        if (!qdone) {
-            const float mb = bv.margin + sr.mo + 1e-5f * bestT;
-            const float mbase = bv.margin + sr.mo;
-            int next = -1, rem = 0, nextRef = 0;
-            float nearT = __builtin_inff();
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                if (!((msk >> c) & 1)) continue;
-                const float4 lo = bv.nodes[8 * cur + 2 * c], hi = bv.nodes[8 * cur + 2 * c + 1];
-                const int cnt = lrt::libm::f2u_i(hi.w);
-                if (cnt < 0) continue;
-                float tn, tf;
-                SlabTest4(lo, hi, o, sr, tn, tf);
-                const float m = __builtin_fmaf(1e-5f, __builtin_fabsf(tf), mbase);   // a margin
-                const float tfm = tf + m;   // (tn <= tf + m, tn <= bestT + mb, tf + m >= kMinT)
-                if (!(tn <= __builtin_fminf(tfm, bestT + mb) && tfm >= kMinT)) continue;
-                if (cnt > 0) {
-                    const int ref = lrt::libm::f2u_i(lo.w);
-                    for (int j = 0; j < cnt; ++j) test(ref + j, bv.lsph[ref + j]);
-                } else {
-                    rem |= 1 << c;
-                    if (tn < nearT) {
-                        nearT = tn;
-                        next = c;
-                        nextRef = lrt::libm::f2u_i(lo.w);
-                    }
-                }
-            }
-            if (next >= 0) {
-                rem &= ~(1 << next);
-                if (rem) {
-                    stk[sp * stride] = (unsigned short)((cur << 4) | rem);
-                    ++sp;
-                }
-                cur = nextRef;
-                msk = 0xF;
-            } else if (sp == 0) {
-                msk = 0;   // this query's traversal is complete
-            } else {   // popped children descend without a second box test (as ClosestHitBVH4)
-                --sp;
-                const int e = stk[sp * stride];
-                cur = e >> 4;
-                msk = e & 0xF;
-                const int c = __builtin_ctz(msk);
-                msk &= msk - 1;
-                if (msk) {
-                    stk[sp * stride] = (unsigned short)((cur << 4) | msk);
-                    ++sp;
-                }
-                cur = lrt::libm::f2u_i(bv.nodes[8 * cur + 2 * c].w);
-                msk = 0xF;
-            }
-            qdone = msk == 0 || (sh && best != -2);
-        }
-        if (qdone) {
-            if (!sh) break;
-            lit = best == -2;   // nothing beat the light
-            // the bounce ray's closest hit from the same origin
-            sh = false;
-            d = db;
-            sr = MakeSlabRay(o, d, bv.margin);
-            bestT = kMaxT;
-            best = -1;
-            for (int j = 0; j < bv.nbig; ++j) test(bv.big0 + j, bv.lsph[bv.big0 + j]);
-            sp = 0;
-            cur = 0;
-            msk = bv.nnodes == 0 ? 0 : 0xF;
+// The traversal is explicit per-lane state (TravQuery) advanced one node visit at a time
+// (TravStep). Shading the lanes whose queries had ended while the others' traversals
+// went on (a pool-kernel variant) kept every lane's TravQuery live across the shading
+// code: 82 VGPRs spilled and config 4 took 404-829 ms instead of 226 (profiles/r2_p2).
+struct TravQuery {
+    F3 o, d, db;   // origin, the current query's direction, the bounce ray's direction
+    SlabRay sr;    // of d
+    float bestT;
+    int best;      // the current winner's position in lsph; -2: the light (index li); -1: none
+    int li;
+    int sp, cur, msk;   // traversal stack depth, node, children still to visit (0: query over)
+    bool sh;            // on the shadow query
+    bool lit;           // the shadow query's answer, once it is over
+    bool busy;          // a query is in progress
+};
+
+LRT_DEV void TravTest(TravQuery& q, const BvhView& bv, int pos, const float4& s) {
+    const F3 rs = f3(s.x, s.y, s.z) - q.o;                       // maths.cpp:54-59
+    const float rsProj = dot(rs, q.d);
+    const float ifHit = dot(rs, rs) - rsProj * rsProj - s.w;
+    if (ifHit < 0.0f) {
+        const float halfCut = sqrt_rn(-ifHit);
+        const float t1 = rsProj - halfCut;
+        const float t2 = rsProj + halfCut;
+        const float cand = t1 > kMinT ? t1 : (t2 > kMinT ? t2 : __builtin_inff());
+        if (cand < q.bestT || (cand == q.bestT && q.best != -1 && bv.lid[pos] < (q.best >= 0 ? bv.lid[q.best] : q.li))) {
+            q.bestT = cand;
+            q.best = pos;
         }
     }
-    tOut = bestT;
-    return best >= 0 ? bv.lid[best] : -1;
+}
+
+// Start the bounce query (d = db): the spheres kept out of the tree first, then the root.
+LRT_DEV void TravStartBounce(TravQuery& q, const BvhView& bv) {
+    q.sh = false;
+    q.d = q.db;
+    q.sr = MakeSlabRay(q.o, q.d, bv.margin);
+    q.bestT = kMaxT;
+    q.best = -1;
+    for (int j = 0; j < bv.nbig; ++j) TravTest(q, bv, bv.big0 + j, bv.lsph[bv.big0 + j]);
+    q.sp = 0;
+    q.cur = 0;
+    q.msk = bv.nnodes == 0 ? 0 : 0xF;
+}
+
+LRT_DEV void TravInit(TravQuery& q, const F3& o, const F3& db, bool hasS, const F3& ds, int li,
+                      const float4& lightSph, const BvhView& bv) {
+    q.o = o;
+    q.db = db;
+    q.li = li;
+    q.lit = false;
+    q.busy = true;
+    const float candL = hasS ? SphereCand(o, ds, lightSph) : kMaxT;
+    if (!(candL < kMaxT)) {   // no shadow ray, or the light is not hit at all: not lit
+        TravStartBounce(q, bv);
+        return;
+    }
+    q.sh = true;
+    q.d = ds;
+    q.sr = MakeSlabRay(o, ds, bv.margin);
+    q.bestT = candL;
+    q.best = -2;
+    for (int j = 0; j < bv.nbig; ++j) TravTest(q, bv, bv.big0 + j, bv.lsph[bv.big0 + j]);
+    q.sp = 0;
+    q.cur = 0;
+    q.msk = bv.nnodes == 0 ? 0 : 0xF;
+}
+
+// One node visit of the lane's current query; at a query's end the shadow query hands over
+// to the bounce query, and the bounce query clears `busy`.
+LRT_DEV void TravStep(TravQuery& q, const BvhView& bv, unsigned short* stk, int stride) {
+    bool qdone = q.msk == 0 || (q.sh && q.best != -2);   // stack exhausted, or the light is beaten
+    if (!qdone) {
+        const float mb = bv.margin + q.sr.mo + 1e-5f * q.bestT;
+        const float mbase = bv.margin + q.sr.mo;
+        int next = -1, rem = 0, nextRef = 0;
+        float nearT = __builtin_inff();
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (!((q.msk >> c) & 1)) continue;
+            const float4 lo = bv.nodes[8 * q.cur + 2 * c], hi = bv.nodes[8 * q.cur + 2 * c + 1];
+            const int cnt = lrt::libm::f2u_i(hi.w);
+            if (cnt < 0) continue;
+            float tn, tf;
+            SlabTest4(lo, hi, q.o, q.sr, tn, tf);
+            const float m = __builtin_fmaf(1e-5f, __builtin_fabsf(tf), mbase);   // a margin
+            const float tfm = tf + m;   // (tn <= tf + m, tn <= bestT + mb, tf + m >= kMinT)
+            if (!(tn <= __builtin_fminf(tfm, q.bestT + mb) && tfm >= kMinT)) continue;
+            if (cnt > 0) {
+                const int ref = lrt::libm::f2u_i(lo.w);
+                for (int j = 0; j < cnt; ++j) TravTest(q, bv, ref + j, bv.lsph[ref + j]);
+            } else {
+                rem |= 1 << c;
+                if (tn < nearT) {
+                    nearT = tn;
+                    next = c;
+                    nextRef = lrt::libm::f2u_i(lo.w);
+                }
+            }
+        }
+        if (next >= 0) {
+            rem &= ~(1 << next);
+            if (rem) {
+                stk[q.sp * stride] = (unsigned short)((q.cur << 4) | rem);
+                ++q.sp;
+            }
+            q.cur = nextRef;
+            q.msk = 0xF;
+        } else if (q.sp == 0) {
+            q.msk = 0;   // this query's traversal is complete
+        } else {   // popped children descend without a second box test (as ClosestHitBVH4)
+            --q.sp;
+            const int e = stk[q.sp * stride];
+            int cur = e >> 4, msk = e & 0xF;
+            const int c = __builtin_ctz(msk);
+            msk &= msk - 1;
+            if (msk) {
+                stk[q.sp * stride] = (unsigned short)((cur << 4) | msk);
+                ++q.sp;
+            }
+            q.cur = lrt::libm::f2u_i(bv.nodes[8 * cur + 2 * c].w);
+            q.msk = 0xF;
+        }
+        qdone = q.msk == 0 || (q.sh && q.best != -2);
+    }
+    if (qdone) {
+        if (q.sh) {
+            q.lit = q.best == -2;   // nothing beat the light
+            TravStartBounce(q, bv);
+        } else {
+            q.busy = false;
+        }
+    }
+}
+
+LRT_DEV int TravResult(const TravQuery& q, const BvhView& bv, float& tOut) {
+    tOut = q.bestT;
+    return q.best >= 0 ? bv.lid[q.best] : -1;
+}
+
+LRT_DEV int ClosestHitDualBVH4(const F3& o, const F3& db, bool hasS, const F3& ds, int li, const float4& lightSph,
+                               const BvhView& bv, float& tOut, bool& lit, unsigned short* stk, int stride) {
+    TravQuery q;
+    TravInit(q, o, db, hasS, ds, li, lightSph, bv);
+    while (q.busy) TravStep(q, bv, stk, stride);
+    lit = q.lit;
+    return TravResult(q, bv, tOut);
 }
 
 // ---- packet (wave-coherent) traversal ----------------------------------------------

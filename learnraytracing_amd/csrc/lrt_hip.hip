@@ -81,7 +81,9 @@ struct KernelArgs {
     int regenMin;                 // v3: ended lanes that trigger a regeneration round
     const float* lerp;            // lerpFac = (float)f / (float)(f + 1) for f < kLerpTable (parallel.cpp:262)
     float4* samp;                 // sample mode: frames planes of xc * rows colours
-    float4* colbuf;               // v5 (pool): kPoolSamples colour slots per block
+    float4* colbuf;               // v5 (pool): poolSlots colour slots per block
+    int poolSlots;
+    int sampOnly;                 // colours only (the pipelined host path): samp is the caller's
 };
 constexpr int kLerpTable = 1 << 16;
 constexpr int kFixedSpheres = 9;   // the reference's kSphereCount (parallel.cpp:27)
@@ -373,13 +375,13 @@ namespace lrt {
 // Sample mode's second half: TraceRowJob's progressive lerp (parallel.cpp:262,280-286)
 // over the frame planes in order, one thread per pixel (coalesced plane reads).
 __global__ void merge_samples_kernel(const float4* __restrict__ samp, float4* __restrict__ out, const float* lerp,
-                                     int npix, int frame0, int frames) {
+                                     int npix, int frame0, int frames, size_t stride) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= npix) return;
     const float4 o = out[i];
     F3 acc = f3(o.x, o.y, o.z);
     for (int k = 0; k < frames; ++k) {
-        const float4 c = samp[(size_t)k * npix + i];
+        const float4 c = samp[(size_t)k * stride + i];
         const int f = frame0 + k;
         const float lerpFac = f < kLerpTable ? lerp[f] : (float)f / (float)(f + 1);
         acc = acc * lerpFac + f3(c.x, c.y, c.z) * (1.0f - lerpFac);
@@ -388,6 +390,26 @@ __global__ void merge_samples_kernel(const float4* __restrict__ samp, float4* __
     d[0] = acc.x;
     d[1] = acc.y;
     d[2] = acc.z;
+}
+
+// The pipelined host path's lerp (render_host_pipelined): prev from device memory (copied
+// there by DMA while the colours were rendered), the result written straight into the
+// caller's page-locked pixels over PCIe (posted writes; no D2H copy command).
+__global__ __launch_bounds__(256) void merge_to_host_kernel(const float4* __restrict__ samp,
+                                                            const float4* __restrict__ prev, float4* host,
+                                                            const float* lerp, int npix, int frame0, int frames,
+                                                            size_t stride) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npix) return;
+    const float4 o = prev[i];
+    F3 acc = f3(o.x, o.y, o.z);
+    for (int k = 0; k < frames; ++k) {   // parallel.cpp:262,282 in frame order
+        const float4 c = samp[(size_t)k * stride + i];
+        const int f = frame0 + k;
+        const float lerpFac = f < kLerpTable ? lerp[f] : (float)f / (float)(f + 1);
+        acc = acc * lerpFac + f3(c.x, c.y, c.z) * (1.0f - lerpFac);
+    }
+    host[i] = make_float4(acc.x, acc.y, acc.z, o.w);   // alpha as read
 }
 
 }  // namespace lrt
@@ -473,6 +495,11 @@ struct Context {
     int bvh_stack_levels = kBvhStackLevels;   // this scene's traversal depth (<= kBvhStackLevels)
 
     float* d_frame = nullptr;   // lrt_draw_test / lrt_render_host staging
+    float4* d_col = nullptr;    // the pipelined host path's sample colours
+    size_t col_bytes = 0;
+    hipStream_t s_in = nullptr;   // its H2D copy stream
+    static constexpr int kHostChunks = 8;
+    hipEvent_t ev_in[kHostChunks] = {};
     float* d_feat[6] = {};      // lrt_render_host_ex feature staging
     size_t feat_bytes[6] = {};
     size_t frame_bytes = 0;
@@ -992,6 +1019,7 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     const int rounds = (a.frames + kSplit - 1) / kSplit;
     const size_t npix = (size_t)xc * rows;
     bool samp = false;
+    if constexpr (!kFeat && kSplit == 1) samp = a.sampOnly && lds && !a.bv.on;
     if constexpr (!kFeat && kSplit >= 4) {
         static int mode = -1;
         if (mode < 0) {
@@ -1002,6 +1030,7 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
         samp = mode > 0 && lds && !a.bv.on && rounds >= 2 && npix * (size_t)a.frames * sizeof(float4) <= (2ull << 30) &&
                (mode == 2 || ntiles < 16 * slots);
     }
+    if (a.sampOnly && !samp) return fail(LRT_E_INVALID, "colours-only render: needs the LDS linear scan, one frame lane");
     const long long tasks = samp ? ntiles * rounds : ntiles;
     long long blocks = (long long)per_cu * cus * LRT_V0_GRID_MULT;
     // block b serves queue b % kV0Queues: every queue that owns a task needs a block, even
@@ -1009,7 +1038,7 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     blocks = std::max(blocks, (long long)kV0Queues);
     if (blocks > tasks) blocks = tasks;
     const dim3 grid((unsigned)blocks);
-    a.samp = nullptr;
+    if (!a.sampOnly) a.samp = nullptr;
     a.ovf = nullptr;
     a.tiles = g_ctx.d_tiles + (size_t)(g_ctx.tiles_next++ % kQueueSlots) * kTileSetU64;
 #ifdef LRT_EXP_SECSTATS
@@ -1024,8 +1053,15 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
         e = hipMallocAsync((void**)&a.ovf, sizeof(float4) * gthreads * (size_t)(a.maxDepth - kTraceLdsLevels), s);
         if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(trace stack overflow)");
     }
-    if constexpr (!kFeat && kSplit >= 4) {
-        if (samp) {
+    if constexpr (!kFeat && (kSplit >= 4 || kSplit == 1)) {
+        if (samp && a.sampOnly) {   // the caller lerps the planes (render_host's pipeline)
+            if (fixed)
+                trace_kernel<MAXD, true, false, kSplit, false, true, kFixedSpheres><<<grid, kBlock, ldsb, s>>>(a);
+            else
+                trace_kernel<MAXD, true, false, kSplit, false, true><<<grid, kBlock, ldsb, s>>>(a);
+            e = hipGetLastError();
+            if (e != hipSuccess) return hip_fail(e, "trace_kernel (colours) launch");
+        } else if (samp) {
             e = hipMallocAsync((void**)&a.samp, sizeof(float4) * npix * (size_t)a.frames, s);
             if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(sample planes)");
             if (fixed)
@@ -1035,7 +1071,7 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
             e = hipGetLastError();
             if (e != hipSuccess) return hip_fail(e, "trace_kernel (samples) launch");
             merge_samples_kernel<<<(unsigned)((npix + 255) / 256), 256, 0, s>>>(a.samp, a.out, a.lerp, (int)npix,
-                                                                               a.frame0, a.frames);
+                                                                               a.frame0, a.frames, npix);
             e = hipGetLastError();
             if (e != hipSuccess) return hip_fail(e, "merge_samples_kernel launch");
             e = hipFreeAsync(a.samp, s);
@@ -1200,7 +1236,17 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     a.ovf = nullptr;
     a.colbuf = nullptr;
     a.tiles = g_ctx.d_tiles + (size_t)(g_ctx.tiles_next++ % kQueueSlots) * kTileSetU64;
-    e = hipMallocAsync((void**)&a.colbuf, sizeof(float4) * kPoolSamples * (size_t)grid.x, s);
+    {   // waiting lanes that trigger a refill (fold + next samples); LRT_POOL_REFILL_MIN
+        static int env = -1;
+        if (env < 0) {
+            const char* v = getenv("LRT_POOL_REFILL_MIN");
+            env = v ? atoi(v) : 0;
+            if (env <= 0 || env > 64) env = 1;
+        }
+        a.regenMin = env;
+    }
+    a.poolSlots = kPix * std::min(a.frames, kPoolSamples / kPix);   // one round's samples
+    e = hipMallocAsync((void**)&a.colbuf, sizeof(float4) * (size_t)a.poolSlots * grid.x, s);
     if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(pool colour slots)");
     if (a.maxDepth > kTraceLdsLevels) {
         const size_t gthreads = (size_t)grid.x * 64;
@@ -1240,9 +1286,10 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
 // Pixels per pool tile: a round holds kPoolSamples samples, so more frames -> fewer pixels.
 template <int MAXD>
 int launch_pool_split(const KernelArgs& a, bool lds, int xc, int rows, int frames, hipStream_t s) {
-    if (frames <= 16) return launch_pool<MAXD, 64>(a, lds, xc, rows, s);
-    if (frames <= 64) return launch_pool<MAXD, 16>(a, lds, xc, rows, s);
-    if (frames <= 256) return launch_pool<MAXD, 4>(a, lds, xc, rows, s);
+    if (64 * frames <= kPoolSamples) return launch_pool<MAXD, 64>(a, lds, xc, rows, s);
+    if (32 * frames <= kPoolSamples) return launch_pool<MAXD, 32>(a, lds, xc, rows, s);
+    if (16 * frames <= kPoolSamples) return launch_pool<MAXD, 16>(a, lds, xc, rows, s);
+    if (4 * frames <= kPoolSamples) return launch_pool<MAXD, 4>(a, lds, xc, rows, s);
     return launch_pool<MAXD, 1>(a, lds, xc, rows, s);
 }
 
@@ -1332,7 +1379,7 @@ int launch_wavefront(KernelArgs a, bool lds, hipStream_t s) {
             }
         }
         merge_samples_kernel<<<(unsigned)((cp + 255) / 256), 256, 0, s>>>(w.samp, a.out + pix0, a.lerp, (int)cp,
-                                                                         a.frame0, a.frames);
+                                                                         a.frame0, a.frames, cp);
         e = hipGetLastError();
         if (e != hipSuccess) return hip_fail(e, "wavefront launch");
     }
@@ -1343,8 +1390,12 @@ int launch_wavefront(KernelArgs a, bool lds, hipStream_t s) {
     return LRT_OK;
 }
 
+int auto_kernel(const KernelArgs& a, const lrt_render_desc* d, bool feat);
+
+// colours_out (render_host's pipeline): no lerp -- frame f's sample colours go to plane
+// f - frame0 of colours_out (x_count * row_count float4 each) and d_buf is not touched.
 int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_rays, const lrt_features* feat,
-                  hipStream_t s) {
+                  hipStream_t s, float4* colours_out = nullptr) {
     int rc = validate(d);
     if (rc) return rc;
     if (!g_ctx.ready) return fail(LRT_E_STATE, "lrt_initialize() has not been called");
@@ -1408,10 +1459,19 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     // state machines (v1/v2/v2s, always slower) were removed and their flags are rejected.
     a.regenMin = 0;
     a.lerp = g_ctx.d_lerp;
+    a.colbuf = nullptr;
+    a.poolSlots = 0;
+    a.samp = colours_out;
+    a.sampOnly = colours_out ? 1 : 0;
+    if (colours_out) {   // v0, one frame lane per pixel, sample mode
+        if (want_feat || !lds || a.bv.on) return fail(LRT_E_INVALID, "colours-only render: LDS linear-scan scenes only");
+        if (d->max_depth <= 8) return launch_depth<8, 1>(a, lds, d->x_count, d->row_count, s);
+        return launch_depth<64, 1>(a, lds, d->x_count, d->row_count, s);
+    }
     if (d->flags & (LRT_F_V1 | LRT_F_V2S | LRT_F_V2))
         return fail(LRT_E_INVALID, "LRT_F_V1/LRT_F_V2S/LRT_F_V2 kernels were removed (use LRT_F_SIMPLE, the default)");
     int kflags = d->flags & (LRT_F_SIMPLE | LRT_F_V3 | LRT_F_WAVEFRONT | LRT_F_POOL);
-    if (kflags == 0) kflags = LRT_F_SIMPLE;
+    if (kflags == 0) kflags = auto_kernel(a, d, want_feat);
     if (want_feat && !(kflags & LRT_F_SIMPLE))
         return fail(LRT_E_INVALID, "features are implemented by the v0 kernel only");
     if (kflags & LRT_F_WAVEFRONT) return launch_wavefront(a, lds, s);
@@ -1428,6 +1488,21 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     // depth 9..64: one instance (MAXD only decides whether stack levels beyond the 8 in LDS
     // exist; 20 and 64 compiled to the same code)
     return launch_split<64>(a, lds, d->x_count, d->row_count, d->frames, want_feat, s);
+}
+
+// The library's kernel policy (measured, profiles/r2_p2): the pool kernel (v5) where paths
+// are long or traversals expensive -- BVH scenes (config 4: 223 vs 303 ms, config 5) and
+// bounce budgets above 8 (config 3: 2.45 vs 2.87 ms) -- given at least 4 frames and two
+// tiles per resident wave; v0 otherwise (config 2: equal, 0.306 ms; few pixels with many
+// frames, a GPU's row shard, take v0's frame lanes and sample mode; features are v0's).
+int auto_kernel(const KernelArgs& a, const lrt_render_desc* d, bool feat) {
+    if (feat || d->frames < 4 || !(a.bv.on || d->max_depth > 8)) return LRT_F_SIMPLE;
+    int pix = 64;
+    while (pix > 1 && pix * d->frames > kPoolSamples) pix /= (pix == 64 || pix == 32 ? 2 : 4);
+    const int tx = pix >= 32 ? 8 : pix >= 8 ? 4 : pix >= 2 ? 2 : 1, ty = pix / tx;
+    const long long tiles = (long long)((d->x_count + tx - 1) / tx) * ((d->row_count + ty - 1) / ty);
+    const long long slots = 16LL * g_ctx.num_cus;   // resident waves (4 per SIMD)
+    return tiles >= 2 * slots ? LRT_F_POOL : LRT_F_SIMPLE;
 }
 
 int ensure_frame(size_t bytes) {
@@ -1466,6 +1541,91 @@ bool host_zero_copy() {
     return on;
 }
 
+// The pipelined host path for page-locked backbuffers (lrt_draw_test at 1280x720 is
+// PCIe-bound). The sample colours do not depend on the buffer's previous values -- only the
+// lerp does (parallel.cpp:282) -- so the colours are rendered into device memory while the
+// previous values travel host -> device by DMA (LRT_HOST_CHUNKS row chunks on a copy
+// stream); each chunk's lerp runs once its copy lands and writes the result straight into
+// the caller's pixels over PCIe, while the next chunk's copy comes the other way. Measured
+// alternatives (profiles/r2_p2): zero copy for the whole render (kernel reads and writes
+// over PCIe, 0.66 ms; GPU-initiated reads and writes share ~64 GB/s); render + one
+// streaming zero-copy lerp (0.70 ms); DMA both ways in 8 chunks (0.72 ms: ~20 us per copy
+// command, and D2H ran as blit kernels). Pageable buffers stay staged (their async copies
+// go through bounce buffers: 1.2 ms pipelined vs 0.77 staged). LRT_HOST_PIPELINE=0: off.
+bool host_pipeline(const lrt_render_desc* d, size_t bytes) {
+    static const int mode = [] {
+        const char* e = getenv("LRT_HOST_PIPELINE");
+        return e ? atoi(e) : 1;
+    }();
+    const bool bvh = g_ctx.bvh_on && !(d->flags & LRT_F_NO_BVH);
+    const bool lds = !(d->flags & LRT_F_SCENE_GLOBAL) &&
+                     sizeof(float4) * (kTraceLdsLevels * kBlock + 4 * (size_t)g_ctx.count + g_ctx.nlights / 4 + 1) <=
+                         64 * 1024;
+    const int kflags = d->flags & (LRT_F_SIMPLE | LRT_F_V3 | LRT_F_WAVEFRONT | LRT_F_POOL);
+    return mode != 0 && d->frames <= 4 && bytes * (size_t)d->frames <= (256u << 20) && !bvh && lds &&
+           (kflags == 0 || kflags == LRT_F_SIMPLE) && !(d->flags & LRT_F_NO_DOUBLE_LIGHT) &&
+           d->row_count >= Context::kHostChunks;
+}
+
+int host_chunks() {   // row chunks of the DMA copy (LRT_HOST_CHUNKS, 1..8)
+    static const int k = [] {
+        const char* e = getenv("LRT_HOST_CHUNKS");
+        const int v = e ? atoi(e) : 2;
+        return v < 1 ? 1 : v > Context::kHostChunks ? Context::kHostChunks : v;
+    }();
+    return k;
+}
+
+int render_host_pipelined(const lrt_render_desc* d, float* buf, float* hdev, size_t bytes, long long* out_rays) {
+    hipStream_t s = g_ctx.stream;
+    if (!g_ctx.s_in) {
+        LRT_HIP(hipStreamCreateWithFlags(&g_ctx.s_in, hipStreamNonBlocking));
+        for (int c = 0; c < Context::kHostChunks; ++c)
+            LRT_HIP(hipEventCreateWithFlags(&g_ctx.ev_in[c], hipEventDisableTiming));
+    }
+    const size_t cbytes = bytes * (size_t)d->frames;
+    if (g_ctx.col_bytes < cbytes) {
+        if (g_ctx.d_col) (void)hipFree(g_ctx.d_col);
+        g_ctx.d_col = nullptr;
+        g_ctx.col_bytes = 0;
+        if (hipMalloc(&g_ctx.d_col, cbytes) != hipSuccess) return fail(LRT_E_NOMEM, "hipMalloc(sample colours)");
+        g_ctx.col_bytes = cbytes;
+    }
+    const int K = host_chunks(), rows = d->row_count, xc = d->x_count;
+    const size_t npix = (size_t)xc * rows;
+    auto chunk = [&](int c, size_t& p0, size_t& n) {   // chunk c: rows [c rows / K, (c + 1) rows / K)
+        const size_t r0 = (size_t)rows * c / K, r1 = (size_t)rows * (c + 1) / K;
+        p0 = r0 * xc;
+        n = (r1 - r0) * xc;
+    };
+    for (int c = 0; c < K; ++c) {   // previous values, host -> device (DMA), beside the render
+        size_t p0, n;
+        chunk(c, p0, n);
+        LRT_HIP(hipMemcpyAsync(g_ctx.d_frame + 4 * p0, buf + 4 * p0, n * 16, hipMemcpyHostToDevice, g_ctx.s_in));
+        LRT_HIP(hipEventRecord(g_ctx.ev_in[c], g_ctx.s_in));
+    }
+    LRT_HIP(hipMemsetAsync(g_ctx.d_rays, 0, sizeof(unsigned long long), s));
+    int rc = render_device(d, g_ctx.d_frame, g_ctx.d_rays, nullptr, s, g_ctx.d_col);
+    if (rc) {
+        (void)hipStreamSynchronize(g_ctx.s_in);
+        return rc;
+    }
+    for (int c = 0; c < K; ++c) {   // each chunk's lerp once its values are in, written to the host pixels
+        size_t p0, n;
+        chunk(c, p0, n);
+        LRT_HIP(hipStreamWaitEvent(s, g_ctx.ev_in[c], 0));
+        merge_to_host_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(
+            g_ctx.d_col + p0, reinterpret_cast<const float4*>(g_ctx.d_frame) + p0, reinterpret_cast<float4*>(hdev) + p0,
+            g_ctx.d_lerp, (int)n, d->frame0, d->frames, npix);
+        LRT_HIP(hipGetLastError());
+    }
+    unsigned long long rays = 0;
+    LRT_HIP(hipMemcpyAsync(&rays, g_ctx.d_rays, sizeof(rays), hipMemcpyDeviceToHost, s));
+    LRT_HIP(hipStreamSynchronize(s));
+    if (out_rays) *out_rays = (long long)rays;
+    return LRT_OK;
+}
+
 int render_host(const lrt_render_desc* d, float* buf, long long* out_rays, const lrt_features* feat = nullptr) {
     int rc = validate(d);
     if (rc) return rc;
@@ -1476,7 +1636,11 @@ int render_host(const lrt_render_desc* d, float* buf, long long* out_rays, const
         if (out_rays) *out_rays = 0;
         return LRT_OK;
     }
-    float* const hdev = (!feat && host_zero_copy()) ? host_pinned(buf) : nullptr;
+    float* hdev = (!feat && host_zero_copy()) ? host_pinned(buf) : nullptr;
+    if (hdev && host_pipeline(d, bytes)) {
+        if ((rc = ensure_frame(bytes))) return rc;
+        return render_host_pipelined(d, buf, hdev, bytes, out_rays);
+    }
     if (hdev) {   // zero copy: the kernel reads and writes the caller's pixels over PCIe
         LRT_HIP(hipMemsetAsync(g_ctx.d_rays, 0, sizeof(unsigned long long), g_ctx.stream));
         if ((rc = render_device(d, hdev, g_ctx.d_rays, nullptr, g_ctx.stream))) return rc;
@@ -1664,6 +1828,10 @@ int lrt_shutdown(void) {
     for (auto* f : g_ctx.d_feat)
         if (f) (void)hipFree(f);
     for (auto& m : g_ctx.masked_streams) (void)hipStreamDestroy(m.first);
+    if (g_ctx.d_col) (void)hipFree(g_ctx.d_col);
+    for (int c = 0; c < Context::kHostChunks; ++c)
+        if (g_ctx.ev_in[c]) (void)hipEventDestroy(g_ctx.ev_in[c]);
+    if (g_ctx.s_in) (void)hipStreamDestroy(g_ctx.s_in);
     if (g_ctx.stream) (void)hipStreamDestroy(g_ctx.stream);
     g_ctx = Context();
     return LRT_OK;

@@ -18,20 +18,26 @@
 // frame-by-frame loop -- and the next round (or tile) starts.
 //
 // Same per-ray arithmetic, RNG streams (PixelSeed(x, y, f)), draw order, ray counting,
-// Scatter and recursion fold as Trace (lrt_trace.h). The colour slots live in global
-// memory (16 KB per resident wave, L2-resident): LDS already holds the recursion stack.
+// Scatter and recursion fold as Trace (lrt_trace.h). The colour slots (16 B per sample of
+// a round) live in global memory: LDS already holds the recursion stack.
 #pragma once
 
 namespace lrt {
 
-constexpr int kPoolSamples = 1024;   // colour slots per wave: samples per round of a tile
-enum : int { kPoolIdle = 0, kPoolTrace = 1, kPoolDone = 2 };
+// Samples per round of a tile, at most: with pixels x frames <= kPoolSamples a tile has one
+// round. Config 4 (64 spp): 1024 (16 px) 229 ms, 2048 (32 px) 222, 4096 (64 px) 221;
+// config 5 (256 spp, one GPU): 1024 (4 px) 3876 ms, 4096 (16 px) 3602 (profiles/r2_p2).
+#ifndef LRT_POOL_SAMPLES
+#define LRT_POOL_SAMPLES 4096
+#endif
+constexpr int kPoolSamples = LRT_POOL_SAMPLES;
+enum : int { kPoolIdle = 0, kPoolTrace = 1, kPoolDone = 2, kPoolEnded = 3 };
 
 template <int kPix>
 struct PoolTile {   // tile shape: kPix pixels, as square as a power of two allows
-    static constexpr int X = kPix >= 64 ? 8 : kPix >= 16 ? 4 : kPix >= 4 ? 2 : 1;
+    static constexpr int X = kPix >= 32 ? 8 : kPix >= 8 ? 4 : kPix >= 2 ? 2 : 1;
     static constexpr int Y = kPix / X;
-    static_assert(X * Y == kPix && kPix <= 64, "kPix: 1, 4, 16 or 64");
+    static_assert(X * Y == kPix && kPix <= 64, "kPix: a power of two up to 64");
 };
 
 template <int MAXD, bool kLds, bool kBvh, int kPix, int kNS = 0>
@@ -98,7 +104,7 @@ __global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const Ker
         if (MAXD <= kTraceLdsLevels || lvl < kTraceLdsLevels) return lstk[lvl * 64];
         return gstk[(size_t)(lvl - kTraceLdsLevels) * gthreads];
     };
-    float4* const slots = a.colbuf + (size_t)blockIdx.x * kPoolSamples;
+    float4* const slots = a.colbuf + (size_t)blockIdx.x * a.poolSlots;   // this wave's colour slots
 
     constexpr int TX = PoolTile<kPix>::X, TY = PoolTile<kPix>::Y;
     constexpr int kRoundFrames = kPoolSamples / kPix;
@@ -144,9 +150,23 @@ __global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const Ker
             dl.l = f3(0.0f, 0.0f, 0.0f);
             dl.contrib = f3(0.0f, 0.0f, 0.0f);
             for (;;) {
-                // ---- refill: lanes without a path take the pool's next samples --------------
-                const unsigned long long needM = __ballot(state == kPoolIdle);
-                if (needM) {
+                // ---- refill: ended paths are folded and their lanes take the pool's next
+                // samples, together once a.regenMin lanes wait (or no path is left to trace),
+                // so the fold and the camera rays run with more lanes than end per bounce ----
+                const unsigned long long waitM = __ballot(state == kPoolIdle || state == kPoolEnded);
+                if (waitM && (__popcll(waitM) >= a.regenMin || __ballot(state == kPoolTrace) == 0)) {
+                    if (state == kPoolEnded) {   // :214 folded leaf-outwards into the sample's slot
+                        sec_count(sc, kSecFold);
+                        F3 T = carry;
+                        for (int d = depth - 1; d >= 0; --d) {
+                            const float4 s = get(d);
+                            const float4 b = sc.mats[3 * __float_as_int(s.w) + 2];
+                            T = f3(s.x, s.y, s.z) + f3(b.x, b.y, b.z) * T;
+                        }
+                        slots[k] = make_float4(T.x, T.y, T.z, 0.0f);
+                        state = kPoolIdle;
+                    }
+                    const unsigned long long needM = waitM;
                     if (state == kPoolIdle) {
                         k = next + __popcll(needM & below);
                         state = kPoolDone;
@@ -174,7 +194,7 @@ __global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const Ker
                 }
                 const unsigned long long traceM = __ballot(state == kPoolTrace);
                 if (traceM == 0) {
-                    if (__ballot(state == kPoolIdle) == 0) break;   // the pool is dry: round done
+                    if (__ballot(state == kPoolIdle || state == kPoolEnded) == 0) break;   // the pool is dry
                     continue;
                 }
                 // camera rays that all start together (a round's first iteration) take the
@@ -245,16 +265,9 @@ __global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const Ker
                             }
                         }
                     }
-                    if (fin) {   // :214 folded leaf-outwards; the colour goes to the sample's slot
-                        sec_count(sc, kSecFold);
-                        F3 T = leaf;
-                        for (int d = depth - 1; d >= 0; --d) {
-                            const float4 s = get(d);
-                            const float4 b = sc.mats[3 * __float_as_int(s.w) + 2];
-                            T = f3(s.x, s.y, s.z) + f3(b.x, b.y, b.z) * T;
-                        }
-                        slots[k] = make_float4(T.x, T.y, T.z, 0.0f);
-                        state = kPoolIdle;
+                    if (fin) {   // the path's leaf colour waits for the fold at the next refill
+                        carry = leaf;
+                        state = kPoolEnded;
                     }
                 }
             }

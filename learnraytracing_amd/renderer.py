@@ -111,8 +111,10 @@ class Job:
 
 def pinned_backbuffer(n_floats: int) -> np.ndarray:
     """A zeroed float32 host array in page-locked memory (a torch pin_memory tensor viewed
-    by numpy; the array keeps the tensor alive). DrawTest / render_host detect such buffers
-    and let the kernel read and write them in place over PCIe (LRT_HOST_ZEROCOPY=0: staged)."""
+    by numpy; the array keeps the tensor alive). DrawTest / render_host detect such buffers:
+    the colours are rendered while the previous values come in by DMA, and the lerp writes
+    the result straight into the buffer over PCIe (LRT_HOST_PIPELINE=0: the kernel reads and
+    writes the buffer in place; LRT_HOST_ZEROCOPY=0: staged like pageable memory)."""
     import torch
     return torch.zeros(int(n_floats), dtype=torch.float32, pin_memory=True).numpy()
 

@@ -55,7 +55,7 @@ def _assert_instance(info, kflags, frames, samp="0"):
     per pixel (v0), or pool_kernel with its tile size for `frames`."""
     assert info["bvh"] == "1" and info["maxd"] == "8", info
     if kflags == POOL:
-        assert info["kernel"] == "pool_kernel" and info["pix"] == str(16 if frames <= 64 else 4), info
+        assert info["kernel"] == "pool_kernel" and info["pix"] == str(64 if frames <= 64 else 16), info
     else:
         assert info["kernel"] == "trace_kernel" and info["split"] == "16" and info["samp"] == samp, info
 
@@ -92,7 +92,9 @@ def test_config4_window_vs_oracle_and_linear_scan(gpu, scene1000, kflags):
 def test_config4_many_tiles_bvh_equals_linear_scan(gpu, scene1000, kflags):
     """Enough 64-spp tiles that the persistent grid refills from its queues several times
     (every block runs many tasks): BVH == linear scan, rays included."""
-    kw = dict(width=3840, height=2160, frames=64, max_depth=8, x0=1536, x_count=768, y0=900, row_count=96)
+    # pool tiles are 8x8 pixels at 64 spp: a larger window for more tiles than blocks
+    xc, yc = (768, 96) if kflags == V0 else (1536, 192)
+    kw = dict(width=3840, height=2160, frames=64, max_depth=8, x0=1536, x_count=xc, y0=900, row_count=yc)
     a, ra, info = _render(gpu, flags=kflags, **kw)
     _assert_instance(info, kflags, 64)
     assert int(info["tasks"]) > int(info["grid"])

@@ -8,7 +8,7 @@
 #   smoke             __graft_entry__.smoke()
 #   bench=C[,ARGS]    bench.py --config C (ARGS: extra bench flags, ';'-separated)
 #   trace=C[,ARGS]    rocprofv3 --kernel-trace --stats of bench.py --config C --streams 1
-#   pmc=C,GROUP       one rocprofv3 --pmc pass (GROUP: fetch | write | sq | sq2) of bench --config C
+#   pmc=C,GROUP[,ARGS] one rocprofv3 --pmc pass (GROUP: fetch | write | sq | sq2) of bench --config C
 #   py=SCRIPT[,ARGS]  python SCRIPT ARGS (diagnostics under tools/)
 #   ab=V,C[,ARGS]     bench.py --config C with LRT_LIB=build_exp/liblrt_V.so (tools/build_variant.sh),
 #                     timed region only (A/B of library variants; V=default: the in-tree library)
@@ -57,8 +57,10 @@ for s in "$@"; do
     trace) run "trace_c${c}_$i" 600 rocprofv3 --kernel-trace --stats -d "$out" -o "trace_c${c}" --output-format csv -- \
              python3 bench.py --config "$c" --steps "$BSTEPS" --streams 1 --no-cpu-baseline $extra ;;
     pmc)   g=${rest%%,*}
+           pextra=""
+           [[ "$rest" == *,* ]] && pextra=${rest#*,}
            run "pmc_c${c}_$g" 300 rocprofv3 --pmc ${PMC[$g]} -d "$out" -o "pmc_c${c}_$g" --output-format csv -- \
-             python3 bench.py --config "$c" --steps 2 --warmup 1 --streams 1 --no-cpu-baseline --no-extra-legs ;;
+             python3 bench.py --config "$c" --steps 2 --warmup 1 --streams 1 --no-cpu-baseline --no-extra-legs ${pextra//;/ } ;;
     py)    run "py$i" 600 python ${val//,/ } ;;
     ab)    c2=${rest%%,*}
            extra2=""

@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
 """Summarise the rocprofv3 output of `tools/gpu.sh trace=C pmc=C,fetch pmc=C,write pmc=C,sq`
-for trace_kernel into profiles/<run>/summary_c<C>.json and register it in
-profiles/pmc_index.json, which bench.py reads for its roofline objects.
+for the render kernel (trace_kernel or pool_kernel, whichever the run launched) into
+profiles/<run>/summary_c<C>.json and register it in profiles/pmc_index.json, which
+bench.py reads for its roofline objects.
 
     python tools/summarize_profile.py gpurun_out/<tag> profiles/<tag> --config C [--key config2_n1]
 
-Per launch of trace_kernel (averaged over the launches of each pass):
+Per launch of the render kernel (averaged over the launches of each pass):
   * counters_per_launch: every collected counter;
   * lane_util = SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU x 64): active lanes per VALU
     instruction (both counters in the same quad-cycle unit);
@@ -26,7 +27,12 @@ import os
 import sys
 from collections import defaultdict
 
-KERNEL = "trace_kernel"
+KERNELS = ("trace_kernel", "pool_kernel")
+KERNEL = None   # the one the profiled run launched (main)
+
+
+def is_render(name):
+    return KERNEL in name if KERNEL else any(k in name for k in KERNELS)
 
 
 def per_launch(files):
@@ -34,7 +40,7 @@ def per_launch(files):
     meta = {}
     for f in files:
         for r in csv.DictReader(open(f)):
-            if KERNEL in r["Kernel_Name"]:
+            if is_render(r["Kernel_Name"]):
                 vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
                 meta = {k: r[k] for k in ("Kernel_Name", "Grid_Size", "Workgroup_Size", "LDS_Block_Size",
                                           "Scratch_Size", "VGPR_Count", "Accum_VGPR_Count", "SGPR_Count") if k in r}
@@ -42,6 +48,7 @@ def per_launch(files):
 
 
 def main():
+    global KERNEL
     prof, out = sys.argv[1], sys.argv[2]
     c = int(sys.argv[sys.argv.index("--config") + 1])
     key = sys.argv[sys.argv.index("--key") + 1] if "--key" in sys.argv else f"config{c}_n1"
@@ -49,7 +56,11 @@ def main():
     summary = {"kernel": KERNEL, "config": c, "key": key,
                "recipe": f"tools/gpu.sh trace={c} pmc={c},fetch pmc={c},write pmc={c},sq"}
     for f in glob.glob(os.path.join(prof, "**", f"trace_c{c}_kernel_stats.csv"), recursive=True):
-        for r in csv.DictReader(open(f)):
+        rows = [r for r in csv.DictReader(open(f)) if is_render(r["Name"])]
+        if rows:   # the render kernel of this run: the one with the most time
+            KERNEL = max(rows, key=lambda r: float(r["Percentage"]))["Name"].split("<")[0].split("::")[-1]
+            summary["kernel"] = KERNEL
+        for r in rows:
             if KERNEL in r["Name"]:
                 summary["kernel_trace"] = {"name": r["Name"], "calls": int(r["Calls"]),
                                            "avg_ns": float(r["AverageNs"]), "min_ns": float(r["MinNs"]),
@@ -62,7 +73,7 @@ def main():
             if line.startswith('{"metric"'):
                 bench_line = json.loads(line)
     for f in glob.glob(os.path.join(prof, "**", f"trace_c{c}_kernel_trace.csv"), recursive=True):
-        rows = sorted((r for r in csv.DictReader(open(f)) if KERNEL in r["Kernel_Name"]),
+        rows = sorted((r for r in csv.DictReader(open(f)) if is_render(r["Kernel_Name"])),
                       key=lambda r: int(r["Start_Timestamp"]))
         if bench_line and bench_line.get("ms_per_launch_alone"):
             a = bench_line["warmup"] + bench_line["steps"]
