@@ -203,7 +203,7 @@ def main():
     import learnraytracing_amd as lrt
     from learnraytracing_amd import _lib as L
     from learnraytracing_amd.dist import gather_to_root, max_shard_rows, shard_rows
-    from learnraytracing_amd.renderer import unshard_tensor
+    from learnraytracing_amd.renderer import pack_rgb_tensor, unshard_rgb_tensor
 
     lrt.InitializeTest()
     # --reserve-cus R: render on a CU-masked stream (lrt_stream_create) leaving R CUs to
@@ -231,7 +231,10 @@ def main():
     nslots = max(2, nstreams)
     bufs = [torch.zeros((max_rows, W, 4), dtype=torch.float32, device=dev) for _ in range(nslots)]
     rays = torch.zeros(1, dtype=torch.int64, device=dev)
-    gathered = [torch.empty((world, max_rows, W, 4), dtype=torch.float32, device=dev) if rank == 0 and world > 1
+    # the exchange carries RGB only (lrt_pack_rgb): 12 of the 16 bytes per pixel cross xGMI
+    packed = [torch.empty((max_rows, W, 3), dtype=torch.float32, device=dev) if world > 1 else None
+              for _ in range(nslots)]
+    gathered = [torch.empty((world, max_rows, W, 3), dtype=torch.float32, device=dev) if rank == 0 and world > 1
                 else None for _ in range(nslots)]
     frames_out = [torch.empty((H, W, 4), dtype=torch.float32, device=dev) if rank == 0 and world > 1 else None
                   for _ in range(nslots)]
@@ -253,7 +256,7 @@ def main():
                 if work is not None:
                     work.wait()   # the assembly stream waits for the gather
                 if rank == 0:
-                    unshard_tensor(gathered[slot], frames_out[slot], W, H, rb, world, astream)
+                    unshard_rgb_tensor(gathered[slot], frames_out[slot], W, H, rb, world, astream)
                 done.record(astream)
         if d2h and rank == 0:
             cstream.wait_event(done if done is not None else rdone)
@@ -275,7 +278,8 @@ def main():
         work = None
         if world > 1:
             with torch.cuda.stream(rs):   # the gather is ordered after this step's render
-                _, work = gather_to_root(bufs[slot], max_rows, world, rank, gathered=gathered[slot], async_op=True)
+                pack_rgb_tensor(bufs[slot], packed[slot], rs)
+                _, work = gather_to_root(packed[slot], max_rows, world, rank, gathered=gathered[slot], async_op=True)
         while pending:
             finish(*pending.pop(0))
         pending.append((work, slot, d2h, rdone))
@@ -326,7 +330,8 @@ def main():
         torch.cuda.synchronize()
         alone_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
         if rank == 0:
-            host = [torch.empty((H, W, 4), dtype=torch.float32, pin_memory=True) for _ in range(nslots)]
+            shape = (H, W, 4) if world > 1 else tuple(bufs[0].shape)   # --shard-of: the shard itself
+            host = [torch.empty(shape, dtype=torch.float32, pin_memory=True) for _ in range(nslots)]
         e2e_steps = max(1, min(args.steps, 10))
         sync_all()
         t2 = time.perf_counter()
@@ -406,7 +411,7 @@ def main():
                             + ("reference 9-sphere scene" if cfg["scene"] == "default" else "random_scene(1000, seed=1)"),
                 "width": W, "height": H, "spp_total": spp_total, "max_depth": D,
                 "rays_per_step": int(rays_per_step),
-                "parallelism": f"rows: row-block-cyclic x{world} (block {rb}), RCCL gather to rank 0"
+                "parallelism": f"rows: row-block-cyclic x{world} (block {rb}), RCCL gather of RGB to rank 0"
                 if world > 1 else ("single GPU" if shards == 1 else
                                    f"DIAGNOSTIC: rank 0's shard of {shards} (block {rb}), no gather"),
                 "scene_reads": "global" if args.scene_global else "LDS-staged",

@@ -228,6 +228,15 @@ int lrt_shard_rows(int height, int row_block, int period, int phase);
 int lrt_unshard_rows(const float* d_src, float* d_dst, int width, int height, int row_block,
                      int period, void* stream);
 
+/* The RGB-only form of the exchange (12 of 16 bytes per pixel cross the interconnect; the
+ * render never writes alpha): lrt_pack_rgb copies npix RGBA quads to packed RGB triples;
+ * lrt_unshard_rows_rgb assembles `period` packed shards of max_rows rows each (shard g at
+ * d_src_rgb + g * max_rows * width * 3) into the RGBA frame, leaving its alpha untouched.
+ * Device pointers, asynchronous on stream. */
+int lrt_pack_rgb(const float* d_rgba, float* d_rgb, long long npix, void* stream);
+int lrt_unshard_rows_rgb(const float* d_src_rgb, float* d_dst, int width, int height, int row_block,
+                         int period, void* stream);
+
 /* Present step (main.cpp:109-141 LinearToSRGB + BGRA8 pack, GDI blit removed):
  * d_rgba (width*height*4 floats) -> d_bgra (width*height uint32, b | g<<8 | r<<16). */
 int lrt_present_bgra8(const float* d_rgba, uint32_t* d_bgra, int width, int height, void* stream);

@@ -114,6 +114,8 @@ SIGNATURES = {
     "lrt_host_free": (_i, [_vp]),
     "lrt_shard_rows": (_i, [_i, _i, _i, _i]),
     "lrt_unshard_rows": (_i, [_vp, _vp, _i, _i, _i, _i, _vp]),
+    "lrt_pack_rgb": (_i, [_vp, _vp, _c.c_longlong, _vp]),
+    "lrt_unshard_rows_rgb": (_i, [_vp, _vp, _i, _i, _i, _i, _vp]),
     "lrt_present_bgra8": (_i, [_vp, _vp, _i, _i, _vp]),
     "lrt_libm_eval_host": (_i, [_i, _vp, _vp, _c.c_longlong]),
     "lrt_libm_eval_device": (_i, [_i, _vp, _vp, _c.c_longlong]),

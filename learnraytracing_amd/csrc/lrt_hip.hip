@@ -428,6 +428,32 @@ __global__ void unshard_kernel(const float4* __restrict__ src, float4* __restric
     dst[(size_t)y * width + x] = src[((size_t)g * maxRows + ly) * width + x];
 }
 
+// The multi-GPU exchange carries RGB only: the shard's alpha is never written by the render
+// (parallel.cpp:283-285) and the frame's own alpha stays where it is, so 12 of the 16 bytes
+// per pixel cross xGMI (precision unchanged).
+__global__ void pack_rgb_kernel(const float4* __restrict__ src, float* __restrict__ dst, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float4 v = src[i];
+    dst[3 * i + 0] = v.x;
+    dst[3 * i + 1] = v.y;
+    dst[3 * i + 2] = v.z;
+}
+__global__ void unshard_rgb_kernel(const float* __restrict__ src, float4* __restrict__ dst, int width, int height,
+                                   int rb, int period, int maxRows) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    if (x >= width || y >= height) return;
+    const int blk = y / rb;
+    const int g = blk % period;
+    const int ly = (blk / period) * rb + y % rb;
+    const float* sp = src + 3 * (((size_t)g * maxRows + ly) * width + x);
+    float* d = reinterpret_cast<float*>(dst + (size_t)y * width + x);   // alpha untouched
+    d[0] = sp[0];
+    d[1] = sp[1];
+    d[2] = sp[2];
+}
+
 // LinearToSRGB + pack (main.cpp:109-141): b | g << 8 | r << 16 per pixel.
 LRT_DEV uint32_t linear_to_srgb(float x) {   // main.cpp:109-115
     x = (x < 0.0f) ? 0.0f : x;                                   // std::max(x, 0.0f)
@@ -1984,6 +2010,27 @@ int lrt_unshard_rows(const float* d_src, float* d_dst, int width, int height, in
     dim3 grid((width + 255) / 256, height);
     unshard_kernel<<<grid, 256, 0, s>>>(reinterpret_cast<const float4*>(d_src), reinterpret_cast<float4*>(d_dst),
                                         width, height, row_block, period, maxRows);
+    LRT_HIP(hipGetLastError());
+    return LRT_OK;
+}
+
+int lrt_pack_rgb(const float* d_rgba, float* d_rgb, long long npix, void* stream) {
+    if (!d_rgba || !d_rgb || npix < 0) return fail(LRT_E_INVALID, "invalid pack arguments");
+    if (npix == 0) return LRT_OK;
+    pack_rgb_kernel<<<(unsigned)((npix + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+        reinterpret_cast<const float4*>(d_rgba), d_rgb, (size_t)npix);
+    LRT_HIP(hipGetLastError());
+    return LRT_OK;
+}
+
+int lrt_unshard_rows_rgb(const float* d_src_rgb, float* d_dst, int width, int height, int row_block, int period,
+                         void* stream) {
+    if (!d_src_rgb || !d_dst || width < 1 || height < 1 || row_block < 1 || period < 1)
+        return fail(LRT_E_INVALID, "invalid unshard arguments");
+    const int maxRows = lrt_shard_rows(height, row_block, period, 0);
+    dim3 grid((width + 255) / 256, height);
+    unshard_rgb_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(d_src_rgb, reinterpret_cast<float4*>(d_dst), width,
+                                                             height, row_block, period, maxRows);
     LRT_HIP(hipGetLastError());
     return LRT_OK;
 }

@@ -202,6 +202,28 @@ def unshard_tensor(gathered, out, width: int, height: int, row_block: int, perio
                                      ctypes.c_void_p(s.cuda_stream)))
 
 
+def pack_rgb_tensor(rgba, rgb, stream=None) -> None:
+    """RGBA quads -> packed RGB triples (lrt_pack_rgb) on cuda tensors: the shard a rank
+    sends in the frame exchange."""
+    import torch
+
+    if rgba.numel() // 4 != rgb.numel() // 3:
+        raise ValueError("pack_rgb: rgba and rgb must hold the same pixels")
+    s = stream if stream is not None else torch.cuda.current_stream(rgba.device)
+    L.check(L.lib().lrt_pack_rgb(ctypes.c_void_p(rgba.data_ptr()), ctypes.c_void_p(rgb.data_ptr()),
+                                 int(rgba.numel() // 4), ctypes.c_void_p(s.cuda_stream)))
+
+
+def unshard_rgb_tensor(gathered_rgb, out, width: int, height: int, row_block: int, period: int, stream=None) -> None:
+    """Frame assembly from packed RGB shards (lrt_unshard_rows_rgb); out's alpha untouched."""
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream(out.device)
+    L.check(L.lib().lrt_unshard_rows_rgb(ctypes.c_void_p(gathered_rgb.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                         int(width), int(height), int(row_block), int(period),
+                                         ctypes.c_void_p(s.cuda_stream)))
+
+
 def present_tensor(rgba, bgra, width: int, height: int, stream=None) -> None:
     """LinearToSRGB + BGRA8 pack (main.cpp:109-141) on cuda tensors."""
     import torch

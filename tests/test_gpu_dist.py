@@ -35,7 +35,7 @@ def _worker(rank, world, port, w, h, rb, frames, depth, outdir):
     torch.cuda.set_device(0)
     import learnraytracing_amd as lrt
     from learnraytracing_amd.dist import gather_to_root, max_shard_rows
-    from learnraytracing_amd.renderer import unshard_tensor
+    from learnraytracing_amd.renderer import pack_rgb_tensor, unshard_rgb_tensor, unshard_tensor
     lrt.InitializeTest()
     try:
         max_rows = max_shard_rows(h, rb, world)
@@ -44,15 +44,21 @@ def _worker(rank, world, port, w, h, rb, frames, depth, outdir):
         job = lrt.Job(width=w, height=h, frames=frames, max_depth=depth, row_block=rb, row_period=world,
                       row_phase=rank)
         lrt.render_tensor(job, local, rays)
+        packed = torch.empty((max_rows, w, 3), dtype=torch.float32, device="cuda")
+        pack_rgb_tensor(local, packed)
         torch.cuda.synchronize()
-        gathered, _ = gather_to_root(local, max_rows, world, rank)
+        gathered, _ = gather_to_root(local, max_rows, world, rank)       # RGBA exchange
+        gathered3, _ = gather_to_root(packed, max_rows, world, rank)     # RGB exchange (bench.py's)
         tot = rays.cpu()
         dist.all_reduce(tot)
         if rank == 0:
             frame = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
             unshard_tensor(gathered, frame, w, h, rb, world)
+            frame3 = torch.full((h, w, 4), 0.5, dtype=torch.float32, device="cuda")
+            unshard_rgb_tensor(gathered3, frame3, w, h, rb, world)
             torch.cuda.synchronize()
             np.save(os.path.join(outdir, "frame.npy"), frame.cpu().numpy())
+            np.save(os.path.join(outdir, "frame3.npy"), frame3.cpu().numpy())
             np.save(os.path.join(outdir, "rays.npy"), tot.numpy())
     finally:
         lrt.ShutdownTest()
@@ -66,9 +72,12 @@ def test_two_rank_gpu_shards_assemble_bitwise(gpu, tmp_path, world, rb, frames):
     mp.start_processes(_worker, args=(world, _free_port(), w, h, rb, frames, depth, str(tmp_path)),
                        nprocs=world, start_method="spawn", join=True)
     frame = np.load(tmp_path / "frame.npy")
+    frame3 = np.load(tmp_path / "frame3.npy")
     want = np.zeros((h, w, 4), np.float32)
     want_rays = gpu.render_host(gpu.Job(width=w, height=h, frames=frames, max_depth=depth), want)
     assert np.array_equal(frame[..., :3].view(np.uint32), want[..., :3].view(np.uint32))
+    assert np.array_equal(frame3[..., :3].view(np.uint32), want[..., :3].view(np.uint32))
+    assert np.all(frame3[..., 3] == 0.5)   # the RGB exchange leaves the frame's alpha alone
     assert int(np.load(tmp_path / "rays.npy")[0]) == want_rays
 
 
