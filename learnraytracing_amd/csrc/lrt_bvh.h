@@ -502,8 +502,10 @@ LRT_DEV bool ShadowReachesLightBVH4(const F3& o, const F3& d, int li, const floa
 // order as ClosestHitBVH4 / ShadowReachesLightBVH4, so both answers are bit-identical.
 // The traversal is explicit per-lane state (TravQuery) advanced one node visit at a time
 // (TravStep). Shading the lanes whose queries had ended while the others' traversals
-// went on (a pool-kernel variant) kept every lane's TravQuery live across the shading
-// code: 82 VGPRs spilled and config 4 took 404-829 ms instead of 226 (profiles/r2_p2).
+// went on (pool-kernel variants) was measured twice and dropped (profiles/r2_p2): with the
+// queries in registers across the shading code 82 VGPRs spilled (config 4: 404-829 ms
+// instead of 226); with the queries saved to memory between a traversal phase and a
+// shading phase still 90 spilled (371-583 ms instead of 224).
 struct TravQuery {
     F3 o, d, db;   // origin, the current query's direction, the bounce ray's direction
     SlabRay sr;    // of d
