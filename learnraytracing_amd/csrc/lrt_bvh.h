@@ -506,6 +506,10 @@ LRT_DEV bool ShadowReachesLightBVH4(const F3& o, const F3& d, int li, const floa
 // queries in registers across the shading code 82 VGPRs spilled (config 4: 404-829 ms
 // instead of 226); with the queries saved to memory between a traversal phase and a
 // shading phase still 90 spilled (371-583 ms instead of 224).
+// LRT_TRAV_UNROLL: unroll factor of TravStep's loop over a node's 4 children (A/B).
+#ifndef LRT_TRAV_UNROLL
+#define LRT_TRAV_UNROLL 4
+#endif
 struct TravQuery {
     F3 o, d, db;   // origin, the current query's direction, the bounce ray's direction
     SlabRay sr;    // of d
@@ -579,7 +583,7 @@ LRT_DEV void TravStep(TravQuery& q, const BvhView& bv, unsigned short* stk, int 
         const float mbase = bv.margin + q.sr.mo;
         int next = -1, rem = 0, nextRef = 0;
         float nearT = __builtin_inff();
-#pragma unroll
+#pragma unroll LRT_TRAV_UNROLL
         for (int c = 0; c < 4; ++c) {
             if (!((q.msk >> c) & 1)) continue;
             const float4 lo = bv.nodes[8 * q.cur + 2 * c], hi = bv.nodes[8 * q.cur + 2 * c + 1];

@@ -1262,12 +1262,14 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     a.ovf = nullptr;
     a.colbuf = nullptr;
     a.tiles = g_ctx.d_tiles + (size_t)(g_ctx.tiles_next++ % kQueueSlots) * kTileSetU64;
-    {   // waiting lanes that trigger a refill (fold + next samples); LRT_POOL_REFILL_MIN
+    {   // waiting lanes that trigger a refill (fold + next samples); LRT_POOL_REFILL_MIN.
+        // Measured (profiles/r2_p2): config 3 2.31 -> 2.05 ms/step at 16 (vs 1), config 4 and
+        // config 2 neutral
         static int env = -1;
         if (env < 0) {
             const char* v = getenv("LRT_POOL_REFILL_MIN");
             env = v ? atoi(v) : 0;
-            if (env <= 0 || env > 64) env = 1;
+            if (env <= 0 || env > 64) env = 16;
         }
         a.regenMin = env;
     }
@@ -1312,9 +1314,13 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
 // Pixels per pool tile: a round holds kPoolSamples samples, so more frames -> fewer pixels.
 template <int MAXD>
 int launch_pool_split(const KernelArgs& a, bool lds, int xc, int rows, int frames, hipStream_t s) {
-    if (64 * frames <= kPoolSamples) return launch_pool<MAXD, 64>(a, lds, xc, rows, s);
-    if (32 * frames <= kPoolSamples) return launch_pool<MAXD, 32>(a, lds, xc, rows, s);
-    if (16 * frames <= kPoolSamples) return launch_pool<MAXD, 16>(a, lds, xc, rows, s);
+    static const int cap = [] {   // LRT_POOL_PIX_MAX: largest tile (A/B)
+        const char* e = getenv("LRT_POOL_PIX_MAX");
+        return e ? atoi(e) : 64;
+    }();
+    if (cap >= 64 && 64 * frames <= kPoolSamples) return launch_pool<MAXD, 64>(a, lds, xc, rows, s);
+    if (cap >= 32 && 32 * frames <= kPoolSamples) return launch_pool<MAXD, 32>(a, lds, xc, rows, s);
+    if (cap >= 16 && 16 * frames <= kPoolSamples) return launch_pool<MAXD, 16>(a, lds, xc, rows, s);
     if (4 * frames <= kPoolSamples) return launch_pool<MAXD, 4>(a, lds, xc, rows, s);
     return launch_pool<MAXD, 1>(a, lds, xc, rows, s);
 }
