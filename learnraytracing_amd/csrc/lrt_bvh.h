@@ -510,6 +510,13 @@ LRT_DEV bool ShadowReachesLightBVH4(const F3& o, const F3& d, int li, const floa
 #ifndef LRT_TRAV_UNROLL
 #define LRT_TRAV_UNROLL 4
 #endif
+// LRT_TRAV_FLAT_LEAVES: the spheres of all leaf children a lane hits in a node are tested in
+// one loop after the box tests (a wave runs max over lanes of their sum) instead of one loop
+// per child slot inside the box-test loop (the sum over slots of each slot's max). Leaf
+// positions must fit 12 bits and counts 1..16 (LRT_MAX_SPHERES <= 4096, leaves <= 16).
+#ifndef LRT_TRAV_FLAT_LEAVES
+#define LRT_TRAV_FLAT_LEAVES 1
+#endif
 struct TravQuery {
     F3 o, d, db;   // origin, the current query's direction, the bounce ray's direction
     SlabRay sr;    // of d
@@ -583,6 +590,7 @@ LRT_DEV void TravStep(TravQuery& q, const BvhView& bv, unsigned short* stk, int 
         const float mbase = bv.margin + q.sr.mo;
         int next = -1, rem = 0, nextRef = 0;
         float nearT = __builtin_inff();
+        uint32_t lmask = 0, lpack0 = 0, lpack1 = 0;   // LRT_TRAV_FLAT_LEAVES: the node's leaves hit
 #pragma unroll LRT_TRAV_UNROLL
         for (int c = 0; c < 4; ++c) {
             if (!((q.msk >> c) & 1)) continue;
@@ -596,13 +604,33 @@ LRT_DEV void TravStep(TravQuery& q, const BvhView& bv, unsigned short* stk, int 
             if (!(tn <= __builtin_fminf(tfm, q.bestT + mb) && tfm >= kMinT)) continue;
             if (cnt > 0) {
                 const int ref = lrt::libm::f2u_i(lo.w);
-                for (int j = 0; j < cnt; ++j) TravTest(q, bv, ref + j, bv.lsph[ref + j]);
+                if (LRT_TRAV_FLAT_LEAVES) {   // leaf position (12 bits) and count - 1 (4 bits)
+                    const uint32_t e = (uint32_t)ref | ((uint32_t)(cnt - 1) << 12);
+                    if (c < 2) lpack0 |= e << (16 * c);
+                    else lpack1 |= e << (16 * (c - 2));
+                    lmask |= 1u << c;
+                } else {
+                    for (int j = 0; j < cnt; ++j) TravTest(q, bv, ref + j, bv.lsph[ref + j]);
+                }
             } else {
                 rem |= 1 << c;
                 if (tn < nearT) {
                     nearT = tn;
                     next = c;
                     nextRef = lrt::libm::f2u_i(lo.w);
+                }
+            }
+        }
+        if (LRT_TRAV_FLAT_LEAVES) {   // one loop over the spheres of every leaf this lane hit
+            int cs = lmask ? __builtin_ctz(lmask) : 0, jj = 0;
+            while (lmask) {
+                const uint32_t e = ((cs < 2 ? lpack0 >> (16 * cs) : lpack1 >> (16 * (cs - 2)))) & 0xFFFFu;
+                const int pos = (int)(e & 4095u) + jj;
+                TravTest(q, bv, pos, bv.lsph[pos]);
+                if (++jj > (int)(e >> 12)) {
+                    lmask &= lmask - 1;
+                    jj = 0;
+                    cs = lmask ? __builtin_ctz(lmask) : 0;
                 }
             }
         }

@@ -11,7 +11,8 @@
 #   pmc=C,GROUP[,ARGS] one rocprofv3 --pmc pass (GROUP: fetch | write | sq | sq2) of bench --config C
 #   py=SCRIPT[,ARGS]  python SCRIPT ARGS (diagnostics under tools/)
 #   ab=V,C[,ARGS]     bench.py --config C with LRT_LIB=build_exp/liblrt_V.so (tools/build_variant.sh),
-#                     timed region only (A/B of library variants; V=default: the in-tree library)
+#                     timed region only (A/B of library variants; V=default: the in-tree library;
+#                     NAME=VALUE tokens in ARGS set environment variables)
 # Output: gpurun_out/$TAG/<step>.log (+ rocprof CSVs).
 cd "$GRAFT_REPO_ROOT" || exit 1
 TAG=${TAG:-latest}
@@ -67,8 +68,12 @@ for s in "$@"; do
            [[ "$rest" == *,* ]] && extra2=${rest#*,}
            lib=build_exp/liblrt_$c.so
            [ "$c" = default ] && lib=learnraytracing_amd/liblrt_hip.so
-           TAILN=1 run "ab_${c}_c${c2}_$i" 600 env LRT_LIB="$lib" python bench.py --config "$c2" --steps "$BSTEPS" \
-             --no-cpu-baseline --no-extra-legs ${extra2//;/ } ;;
+           envs=() bargs=()   # ARGS tokens NAME=VALUE are environment settings (e.g. LRT_BVH_LEAF=8)
+           for tok in ${extra2//;/ }; do
+             if [[ "$tok" =~ ^[A-Z_][A-Z0-9_]*= ]]; then envs+=("$tok"); else bargs+=("$tok"); fi
+           done
+           TAILN=1 run "ab_${c}_c${c2}_$i" 600 env LRT_LIB="$lib" "${envs[@]}" python bench.py --config "$c2" \
+             --steps "$BSTEPS" --no-cpu-baseline --no-extra-legs "${bargs[@]}" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
