@@ -84,20 +84,6 @@ struct KernelArgs {
     float4* colbuf;               // v5 (pool): poolSlots colour slots per block
     int poolSlots;
     int sampOnly;                 // colours only (the pipelined host path): samp is the caller's
-    // Fused host lerp (render_host's page-locked DrawTest path, one frame, kSamp): `out` is
-    // the device copy of the caller's previous values, arriving by DMA in `chunks` row
-    // chunks while the kernel runs; the host thread counts landed chunks in *landed (from
-    // landedBase, page-locked host memory). The grid's first `pollers` blocks copy that
-    // count into the kMirrors device-memory `mirror` words; a render wave waits on a mirror
-    // word for its rows' chunk, lerps and writes hostOut (the caller's pixels, over PCIe).
-    // *hostErr = 1 if a wait timed out.
-    float4* hostOut;
-    const unsigned* landed;
-    unsigned landedBase;
-    int chunks;
-    unsigned* hostErr;
-    unsigned* mirror;
-    int pollers;
 };
 constexpr int kLerpTable = 1 << 16;
 constexpr int kFixedSpheres = 9;   // the reference's kSphereCount (parallel.cpp:27)
@@ -147,78 +133,6 @@ __device__ void block_epilogue(unsigned long long* tiles, unsigned long long* ra
     }
 }
 
-// Fused host lerp (KernelArgs::hostOut). Row ly's values arrive with chunk
-// ((ly + 1) * chunks - 1) / rows (chunk c holds rows [rows * c / chunks, rows * (c + 1) / chunks),
-// as render_host_fused copies them). The count of landed chunks is polled from page-locked
-// host memory (uncached on the GPU) with the wave's loop wave-uniform; a wait has a bound
-// (kHostWaitTicks of the 100 MHz real-time counter), after which the wave reports the timeout
-// and goes on, so the grid always drains.
-constexpr unsigned long long kHostWaitTicks = 20000000ull;   // 200 ms
-constexpr int kMirrors = 64, kMirrorStride = 64;   // copies of the landed count, 256 B apart
-constexpr int kHostPollers = 8;
-// Render waves poll device memory (one of kMirrors copies, so no single address takes
-// every wave's loads); only the poller waves read the host word, so the polling costs
-// PCIe a few requests per microsecond instead of one per waiting wave.
-__device__ __forceinline__ void host_wait_rows(const KernelArgs& a, int ly, int bid, int& seen) {
-    const int need = ((ly + 1) * a.chunks - 1) / a.rows + 1;
-    if (need <= seen) return;
-    const unsigned* m = a.mirror + (bid % kMirrors) * kMirrorStride;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
-        const unsigned v = __hip_atomic_load(m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const int got = __builtin_amdgcn_readfirstlane((int)(v - a.landedBase));
-        if (got >= need) {
-            seen = got;
-            return;
-        }
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kHostWaitTicks) {
-            if ((threadIdx.x & 63) == 0) __hip_atomic_store(a.hostErr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            seen = a.chunks;   // give up: the call reports the error
-            return;
-        }
-        __builtin_amdgcn_s_sleep(16);
-    }
-}
-// Poller wave p (of a.pollers): copies the host's landed count into its share of the
-// mirror words until every chunk is in (or the bound passes: then it releases the render
-// waves itself, and the call reports the timeout).
-__device__ void host_poller(const KernelArgs& a, int p) {
-    const int lane = threadIdx.x & 63;
-    const int per = kMirrors / a.pollers;
-    unsigned* m = a.mirror + (p * per + lane) * kMirrorStride;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    int last = -1;
-    for (;;) {
-        const unsigned v = __hip_atomic_load(a.landed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        int got = __builtin_amdgcn_readfirstlane((int)(v - a.landedBase));
-        const bool late = __builtin_amdgcn_s_memrealtime() - t0 > kHostWaitTicks;
-        if (late) {
-            if (lane == 0) __hip_atomic_store(a.hostErr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            got = a.chunks;
-        }
-        if (got != last && got >= 0) {
-            if (lane < per) __hip_atomic_store(m, a.landedBase + (unsigned)got, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            last = got;
-        }
-        if (got >= a.chunks) return;
-        __builtin_amdgcn_s_sleep(2);
-    }
-}
-// merge_to_host_kernel's lerp for one frame: the previous value is read past the caches
-// (system-scope loads: the DMA wrote it while this kernel ran), the result goes to the
-// caller's pixel with the alpha as read.
-__device__ __forceinline__ void host_lerp_store(const KernelArgs& a, size_t pix, int f, F3 c) {
-    const unsigned* pv = reinterpret_cast<const unsigned*>(a.out + pix);
-    float4 o;
-    o.x = __builtin_bit_cast(float, __hip_atomic_load(pv + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-    o.y = __builtin_bit_cast(float, __hip_atomic_load(pv + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-    o.z = __builtin_bit_cast(float, __hip_atomic_load(pv + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-    o.w = __builtin_bit_cast(float, __hip_atomic_load(pv + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-    const float lerpFac = f < kLerpTable ? a.lerp[f] : (float)f / (float)(f + 1);   // parallel.cpp:262
-    const F3 acc = f3(o.x, o.y, o.z) * lerpFac + c * (1.0f - lerpFac);                 // :282
-    a.hostOut[pix] = make_float4(acc.x, acc.y, acc.z, o.w);
-}
-
 // 4 waves per SIMD: caps VGPRs at 128. The MAXD 20/64 and BVH instances otherwise
 // take 129-144 and drop to 3 waves (config 3: 4.44 -> 4.15 ms, config 4: 587 -> 538 ms
 // with the cap; the BVH instances spill 28-40 B/lane to scratch, which costs less).
@@ -247,13 +161,6 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
     static_assert(kNS == 0 || (kLds && !kBvh), "a fixed sphere count is for the LDS linear scan");
     static_assert(!kFeat || kSplit == 1, "feature launches keep a pixel's frames on one lane");
     static_assert(!(kFeat && kSamp), "sample mode has no features");
-    // fused host lerp: the first a.pollers blocks relay the host's copy count (host_poller)
-    const int pollers = kSamp ? a.pollers : 0;
-    if (kSamp && (int)blockIdx.x < pollers) {
-        host_poller(a, blockIdx.x);
-        return;
-    }
-    const int bid = (int)blockIdx.x - pollers, nblk = (int)gridDim.x - pollers;   // render blocks
     // LDS: [recursion stack kTraceLdsLevels x kBlock][powf tables][spheres][materials][lights][bvh stack]
     extern __shared__ float4 smem[];
     const int tid = threadIdx.x;
@@ -326,12 +233,11 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
     const float invHeight = 1.0f / (float)a.height;   // parallel.cpp:261
     const int fend = a.frame0 + a.frames;
     int rays = 0;
-    int landedSeen = 0;   // fused host lerp: chunks this wave knows have landed
-    const int q = bid % kV0Queues;
-    const int bq = (nblk - q + kV0Queues - 1) / kV0Queues;   // blocks serving queue q
-    const int nq = (ntiles - q + kV0Queues - 1) / kV0Queues;  // tiles owned by queue q
+    const int q = blockIdx.x % kV0Queues;
+    const int bq = ((int)gridDim.x - q + kV0Queues - 1) / kV0Queues;   // blocks serving queue q
+    const int nq = (ntiles - q + kV0Queues - 1) / kV0Queues;            // tiles owned by queue q
     unsigned long long* ctr = a.tiles + q * kCtrStride;
-    for (int i = bid / kV0Queues; i < nq;) {
+    for (int i = blockIdx.x / kV0Queues; i < nq;) {
         // Block b starts on its queue's tile b / kV0Queues; later tiles come from the
         // queue's counter (re-armed by the queue's last block, block_epilogue). The fetch is
         // issued after this tile's loads (vmcnt retires in order, so a load issued behind
@@ -371,13 +277,8 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
                                                gthreads, a.ndl, feat);
             }
             if constexpr (kSamp) {   // the merge kernel lerps the planes in frame order
-                if (a.hostOut) {   // ... or this wave does, once its rows' previous values are in
-                    const int wly = (tile / tilesX) * kTileRows + (wave / kBlockWavesX) * kWaveRows + kWaveRows - 1;
-                    host_wait_rows(a, wly < a.rows ? wly : a.rows - 1, bid, landedSeen);
-                    if (valid && f < fend) host_lerp_store(a, pix, f, col);
-                } else if (valid && f < fend) {
+                if (valid && f < fend)
                     a.samp[(size_t)(f - a.frame0) * ((size_t)a.xc * a.rows) + pix] = make_float4(col.x, col.y, col.z, 0.0f);
-                }
                 continue;
             }
             // the group's colours go through this lane's (now free) stack level 0 in LDS:
@@ -625,12 +526,6 @@ struct Context {
     hipStream_t s_in = nullptr;   // its H2D copy stream
     static constexpr int kHostChunks = 8;
     hipEvent_t ev_in[kHostChunks] = {};
-    unsigned* h_sync = nullptr;   // fused host lerp: [0] landed chunks, [1] wait timeout (coherent page-locked)
-    unsigned* d_sync = nullptr;   // its device address
-    unsigned sync_base = 0;
-    unsigned* d_mirror = nullptr;   // fused host lerp: kMirrors copies of the count (fine-grained)
-    float* d_prev = nullptr;        // fused host lerp: the previous values' copy (fine-grained)
-    size_t prev_bytes = 0;
     float* d_feat[6] = {};      // lrt_render_host_ex feature staging
     size_t feat_bytes[6] = {};
     size_t frame_bytes = 0;
@@ -1163,14 +1058,12 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     }
     if (a.sampOnly && !samp) return fail(LRT_E_INVALID, "colours-only render: needs the LDS linear scan, one frame lane");
     const long long tasks = samp ? ntiles * rounds : ntiles;
-    // fused host lerp: kHostPollers poller blocks first, in slots taken from the render's
-    a.pollers = (samp && a.hostOut) ? kHostPollers : 0;
-    long long blocks = (long long)per_cu * cus * LRT_V0_GRID_MULT - a.pollers;
+    long long blocks = (long long)per_cu * cus * LRT_V0_GRID_MULT;
     // block b serves queue b % kV0Queues: every queue that owns a task needs a block, even
     // on a CU-masked stream left with fewer slots than queues (those blocks start later)
     blocks = std::max(blocks, (long long)kV0Queues);
     if (blocks > tasks) blocks = tasks;
-    const dim3 grid((unsigned)(blocks + a.pollers));
+    const dim3 grid((unsigned)blocks);
     if (!a.sampOnly) a.samp = nullptr;
     a.ovf = nullptr;
     a.tiles = g_ctx.d_tiles + (size_t)(g_ctx.tiles_next++ % kQueueSlots) * kTileSetU64;
@@ -1531,21 +1424,10 @@ int launch_wavefront(KernelArgs a, bool lds, hipStream_t s) {
 
 int auto_kernel(const KernelArgs& a, const lrt_render_desc* d, bool feat);
 
-struct HostLerp {   // render_host_fused's side of KernelArgs::hostOut
-    float4* out;
-    const unsigned* landed;
-    unsigned base;
-    int chunks;
-    unsigned* err;
-    unsigned* mirror;
-};
-
 // colours_out (render_host's pipeline): no lerp -- frame f's sample colours go to plane
 // f - frame0 of colours_out (x_count * row_count float4 each) and d_buf is not touched.
-// hl (render_host_fused, one frame): d_buf holds the previous values as they land, the
-// lerped pixels go to hl->out.
 int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_rays, const lrt_features* feat,
-                  hipStream_t s, float4* colours_out = nullptr, const HostLerp* hl = nullptr) {
+                  hipStream_t s, float4* colours_out = nullptr) {
     int rc = validate(d);
     if (rc) return rc;
     if (!g_ctx.ready) return fail(LRT_E_STATE, "lrt_initialize() has not been called");
@@ -1612,17 +1494,8 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     a.colbuf = nullptr;
     a.poolSlots = 0;
     a.samp = colours_out;
-    a.sampOnly = (colours_out || hl) ? 1 : 0;
-    a.hostOut = hl ? hl->out : nullptr;
-    a.landed = hl ? hl->landed : nullptr;
-    a.landedBase = hl ? hl->base : 0u;
-    a.chunks = hl ? hl->chunks : 0;
-    a.hostErr = hl ? hl->err : nullptr;
-    a.mirror = hl ? hl->mirror : nullptr;
-    a.pollers = 0;   // launch_depth's
-    if (hl && (d->frames != 1 || hl->chunks < 1 || !hl->out || !hl->landed || !hl->err || !hl->mirror))
-        return fail(LRT_E_INVALID, "fused host lerp: one frame and a chunk count");
-    if (a.sampOnly) {   // v0, one frame lane per pixel, sample mode
+    a.sampOnly = colours_out ? 1 : 0;
+    if (colours_out) {   // v0, one frame lane per pixel, sample mode
         if (want_feat || !lds || a.bv.on) return fail(LRT_E_INVALID, "colours-only render: LDS linear-scan scenes only");
         if (d->max_depth <= 8) return launch_depth<8, 1>(a, lds, d->x_count, d->row_count, s);
         return launch_depth<64, 1>(a, lds, d->x_count, d->row_count, s);
@@ -1785,106 +1658,6 @@ int render_host_pipelined(const lrt_render_desc* d, float* buf, float* hdev, siz
     return LRT_OK;
 }
 
-// The fused host path (one frame per call -- DrawTest -- on a page-locked buffer): the
-// previous values travel host -> device by DMA in row chunks, as in the pipelined path,
-// but the render kernel itself lerps and writes each wave's pixels to the caller's buffer
-// once that wave's chunk is in (KernelArgs::hostOut), so the PCIe writes run during the
-// render instead of after it. This host thread relays the copy events to the kernel: it
-// spins on each chunk's event and then bumps the landed count in coherent page-locked
-// memory, which the waves poll. The kernel's waits are bounded (a timeout fails the call),
-// and the count always reaches its end, so the grid drains whatever happens.
-// LRT_HOST_FUSED=1 selects it (off by default: measured slower); LRT_HOST_CHUNKS
-// sets the chunks (default 4).
-bool host_fused() {
-    static const bool on = [] {
-        const char* e = getenv("LRT_HOST_FUSED");
-        return e && atoi(e) != 0;
-    }();
-    return on;
-}
-
-int render_host_fused(const lrt_render_desc* d, float* buf, float* hdev, size_t bytes, long long* out_rays) {
-    hipStream_t s = g_ctx.stream;
-    if (!g_ctx.s_in) {
-        LRT_HIP(hipStreamCreateWithFlags(&g_ctx.s_in, hipStreamNonBlocking));
-        for (int c = 0; c < Context::kHostChunks; ++c)
-            LRT_HIP(hipEventCreateWithFlags(&g_ctx.ev_in[c], hipEventDisableTiming));
-    }
-    if (!g_ctx.h_sync) {
-        void* p = nullptr;
-        if (hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
-            return fail(LRT_E_NOMEM, "hipHostMalloc(copy flags)");
-        void* dp = nullptr;
-        if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess) {
-            (void)hipHostFree(p);
-            return fail(LRT_E_HIP, "hipHostGetDevicePointer(copy flags)");
-        }
-        g_ctx.h_sync = static_cast<unsigned*>(p);
-        g_ctx.d_sync = static_cast<unsigned*>(dp);
-        __atomic_store_n(&g_ctx.h_sync[0], 0u, __ATOMIC_RELEASE);
-    }
-    // Fine-grained device memory for what the kernel reads while others write it: the
-    // mirror words (poller waves) and the previous values (the DMA).
-    if (!g_ctx.d_mirror) {
-        const size_t mb = sizeof(unsigned) * kMirrors * kMirrorStride;
-        if (hipExtMallocWithFlags((void**)&g_ctx.d_mirror, mb, hipDeviceMallocFinegrained) != hipSuccess) {
-            g_ctx.d_mirror = nullptr;
-            return fail(LRT_E_NOMEM, "hipExtMallocWithFlags(copy count mirror)");
-        }
-        LRT_HIP(hipMemset(g_ctx.d_mirror, 0, mb));
-    }
-    if (g_ctx.prev_bytes < bytes) {
-        if (g_ctx.d_prev) (void)hipFree(g_ctx.d_prev);
-        g_ctx.d_prev = nullptr;
-        g_ctx.prev_bytes = 0;
-        if (hipExtMallocWithFlags((void**)&g_ctx.d_prev, bytes, hipDeviceMallocFinegrained) != hipSuccess) {
-            g_ctx.d_prev = nullptr;
-            return fail(LRT_E_NOMEM, "hipExtMallocWithFlags(previous values)");
-        }
-        g_ctx.prev_bytes = bytes;
-    }
-    static const int K = [] {
-        const char* e = getenv("LRT_HOST_CHUNKS");
-        const int v = e ? atoi(e) : 4;
-        return v < 1 ? 1 : v > Context::kHostChunks ? Context::kHostChunks : v;
-    }();
-    const int rows = d->row_count, xc = d->x_count;
-    const unsigned base = (g_ctx.sync_base += 16u);   // this call's counts: base + 1 .. base + K
-    __atomic_store_n(&g_ctx.h_sync[1], 0u, __ATOMIC_RELAXED);
-    for (int c = 0; c < K; ++c) {   // previous values, host -> device (DMA), beside the render
-        const size_t r0 = (size_t)rows * c / K, r1 = (size_t)rows * (c + 1) / K;
-        LRT_HIP(hipMemcpyAsync(g_ctx.d_prev + 4 * r0 * xc, buf + 4 * r0 * xc, (r1 - r0) * xc * 16,
-                               hipMemcpyHostToDevice, g_ctx.s_in));
-        LRT_HIP(hipEventRecord(g_ctx.ev_in[c], g_ctx.s_in));
-    }
-    LRT_HIP(hipMemsetAsync(g_ctx.d_rays, 0, sizeof(unsigned long long), s));
-    const HostLerp hl{reinterpret_cast<float4*>(hdev), g_ctx.d_sync, base, K, g_ctx.d_sync + 1, g_ctx.d_mirror};
-    int rc = render_device(d, g_ctx.d_prev, g_ctx.d_rays, nullptr, s, nullptr, &hl);
-    hipError_t copy_err = hipSuccess;
-    for (int c = 0; c < K; ++c) {   // relay: chunk c is in device memory -> tell the waves
-        hipError_t e;
-        while ((e = hipEventQuery(g_ctx.ev_in[c])) == hipErrorNotReady) {
-        }
-        if (e != hipSuccess && copy_err == hipSuccess) copy_err = e;
-        __atomic_store_n(&g_ctx.h_sync[0], base + (unsigned)c + 1u, __ATOMIC_RELEASE);
-    }
-    if (rc) {
-        (void)hipStreamSynchronize(s);
-        return rc;
-    }
-    if (copy_err != hipSuccess) {
-        (void)hipStreamSynchronize(s);
-        return hip_fail(copy_err, "hipMemcpyAsync(previous values)");
-    }
-    unsigned long long rays = 0;
-    LRT_HIP(hipMemcpyAsync(&rays, g_ctx.d_rays, sizeof(rays), hipMemcpyDeviceToHost, s));
-    LRT_HIP(hipStreamSynchronize(s));
-    if (__atomic_load_n(&g_ctx.h_sync[1], __ATOMIC_ACQUIRE))
-        return fail(LRT_E_HIP, "fused host lerp: timed out waiting for a row chunk's copy");
-    if (out_rays) *out_rays = (long long)rays;
-    return LRT_OK;
-}
-
 int render_host(const lrt_render_desc* d, float* buf, long long* out_rays, const lrt_features* feat = nullptr) {
     int rc = validate(d);
     if (rc) return rc;
@@ -1898,7 +1671,6 @@ int render_host(const lrt_render_desc* d, float* buf, long long* out_rays, const
     float* hdev = (!feat && host_zero_copy()) ? host_pinned(buf) : nullptr;
     if (hdev && host_pipeline(d, bytes)) {
         if ((rc = ensure_frame(bytes))) return rc;
-        if (d->frames == 1 && host_fused()) return render_host_fused(d, buf, hdev, bytes, out_rays);
         return render_host_pipelined(d, buf, hdev, bytes, out_rays);
     }
     if (hdev) {   // zero copy: the kernel reads and writes the caller's pixels over PCIe
@@ -2092,9 +1864,6 @@ int lrt_shutdown(void) {
     for (int c = 0; c < Context::kHostChunks; ++c)
         if (g_ctx.ev_in[c]) (void)hipEventDestroy(g_ctx.ev_in[c]);
     if (g_ctx.s_in) (void)hipStreamDestroy(g_ctx.s_in);
-    if (g_ctx.h_sync) (void)hipHostFree(g_ctx.h_sync);
-    if (g_ctx.d_mirror) (void)hipFree(g_ctx.d_mirror);
-    if (g_ctx.d_prev) (void)hipFree(g_ctx.d_prev);
     if (g_ctx.stream) (void)hipStreamDestroy(g_ctx.stream);
     g_ctx = Context();
     return LRT_OK;

@@ -1,10 +1,9 @@
 """The reference API's host-buffer paths (lrt_draw_test / lrt_render_host, parallel.cpp:297-323)
 under each of their implementations, in fresh processes (the path switches are read once
-per process): for page-locked buffers the fused path (previous values copied in by DMA in
-row chunks while the render kernel runs; each wave lerps and writes its pixels to the
-host once its chunk is in; LRT_HOST_FUSED=1; 1, 3, 4 and 8 chunks) and the pipelined one (the default:
-colours rendered beside the copies, then a chunked lerp written to the host pixels), zero
-copy (LRT_HOST_PIPELINE=0), and the staged path for pageable buffers. Every one must give the oracle's bits and ray counts over several progressive
+per process): the pipelined path for page-locked buffers (colours rendered while the
+previous values are copied in by DMA, chunked lerp written straight to the host pixels;
+1, 3 and 8 row chunks), zero copy (LRT_HOST_PIPELINE=0), and the staged path for pageable
+buffers. Every one must give the oracle's bits and ray counts over several progressive
 frames, with the caller's alpha untouched."""
 import os
 import subprocess
@@ -41,17 +40,13 @@ print("ok")
 
 
 @pytest.mark.parametrize("env,pinned,w,h", [
-    ({"LRT_HOST_FUSED": "1"}, True, 200, 117),           # fused, 4 chunks
-    ({"LRT_HOST_FUSED": "1", "LRT_HOST_CHUNKS": "1"}, True, 160, 90),
-    ({"LRT_HOST_FUSED": "1", "LRT_HOST_CHUNKS": "3"}, True, 200, 117),   # uneven chunks
-    ({"LRT_HOST_FUSED": "1", "LRT_HOST_CHUNKS": "8"}, True, 96, 61),
-    ({"LRT_HOST_FUSED": "1"}, True, 1280, 720),          # the DrawTest size
     ({}, True, 200, 117),                                # pipelined, 2 chunks (default)
-    ({"LRT_HOST_CHUNKS": "3"}, True, 200, 117),
+    ({"LRT_HOST_CHUNKS": "1"}, True, 160, 90),
+    ({"LRT_HOST_CHUNKS": "3"}, True, 200, 117),          # uneven chunks
     ({"LRT_HOST_CHUNKS": "8"}, True, 96, 61),
     ({"LRT_HOST_PIPELINE": "0"}, True, 200, 117),        # zero copy
     ({}, False, 200, 117),                               # pageable: staged
-], ids=["fused4", "fused1", "fused3", "fused8", "fused4_720p", "pipe2", "pipe3", "pipe8", "zerocopy", "pageable"])
+], ids=["pipe2", "pipe1", "pipe3", "pipe8", "zerocopy", "pageable"])
 def test_drawtest_host_paths(env, pinned, w, h):
     code = SCRIPT.format(root=ROOT, oracle=os.path.join(ROOT, "oracle"), w=w, h=h, pinned=pinned)
     p = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), capture_output=True, text=True,

@@ -8,7 +8,7 @@
 #   smoke             __graft_entry__.smoke()
 #   bench=C[,ARGS]    bench.py --config C (ARGS: extra bench flags, ';'-separated)
 #   trace=C[,ARGS]    rocprofv3 --kernel-trace --stats of bench.py --config C --streams 1
-#   pmc=C,GROUP[,ARGS] one rocprofv3 --pmc pass (GROUP: fetch | write | sq | sq2) of bench --config C
+#   pmc=C,GROUP[,ARGS] one rocprofv3 --pmc pass (GROUP: fetch | write | sq | sq2 | cache) of bench --config C
 #   py=SCRIPT[,ARGS]  python SCRIPT ARGS (diagnostics under tools/)
 #   ab=V,C[,ARGS]     bench.py --config C with LRT_LIB=build_exp/liblrt_V.so (tools/build_variant.sh),
 #                     timed region only (A/B of library variants; V=default: the in-tree library;
@@ -25,6 +25,7 @@ declare -A PMC=(
   [write]="WRITE_SIZE"
   [sq]="SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_ANY"
   [sq2]="SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM"
+  [cache]="TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum"
 )
 run() {   # run NAME SECONDS CMD...
   local name=$1 t=$2
