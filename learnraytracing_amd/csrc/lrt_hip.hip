@@ -83,6 +83,8 @@ struct KernelArgs {
     float4* samp;                 // sample mode: frames planes of xc * rows colours
     float4* colbuf;               // v5 (pool): poolSlots colour slots per block
     int poolSlots;
+    const int* perm;              // v5: queue position -> tile, heaviest measured tiles first (null: identity)
+    unsigned* tcost;              // v5: per-tile cost recording (100 MHz ticks of the tile's wave), or null
     int sampOnly;                 // colours only (the pipelined host path): samp is the caller's
 };
 constexpr int kLerpTable = 1 << 16;
@@ -504,6 +506,18 @@ struct Context {
         unsigned long long* rayp = nullptr;  // 16 ray-count partials
     } wf;
     unsigned tiles_next = 0;
+    unsigned scene_version = 0;   // bumped by every scene upload (tile-order signatures)
+    // The pool kernel's tile order for the last render signature seen (tile_order()):
+    // per-tile costs recorded by one launch, then a heaviest-first permutation for the rest.
+    struct TileOrder {
+        uint64_t sig = 0;
+        long long ntiles = 0;
+        int state = 0;                 // 0: none, 1: costs being recorded, 2: permutation ready
+        unsigned* d_cost = nullptr;
+        int* d_perm = nullptr;
+        hipEvent_t ev = nullptr;       // the recording launch's end
+        std::vector<int> h_perm;       // the upload's source (kept alive)
+    } order;
     hipStream_t stream = nullptr;
     int count = 0, nlights = 0;
     float4* d_sph = nullptr;
@@ -887,6 +901,7 @@ int upload_scene(Context& c, const lrt_sphere* s, const lrt_material* m, int n) 
         c.bvh_on = 1;
     }
     c.count = n;
+    ++c.scene_version;
     c.nlights = (int)lights.size();
     c.spheres.assign(s, s + n);
     c.mats.assign(m, m + n);
@@ -1234,6 +1249,76 @@ int launch_regen_split(const KernelArgs& a, bool lds, int xc, int rows, int fram
 
 // v5 (lrt_pool.h): v0's LDS layout, queues, counters and overflow stack, plus the
 // per-block colour slots.
+// Heaviest-first tile order for the pool kernel (LRT_POOL_ORDER=0: off). A pool tile is
+// 4x a v0 task, and a tile over a glass sphere costs several average ones, so a launch in
+// queue order ends with a few waves finishing heavy tiles while the rest of the chip idles
+// (profiles/r2_p8). The first launch of a render signature (window, frames, depth, flags,
+// camera, scene, tile size) records each tile's cost; once it has finished, the next launch
+// of that signature sorts the costs on the host and hands tiles out heaviest first -- the
+// classic LPT order -- and so does every later one. Each pixel's result is unchanged: only
+// the order in which tiles are taken changes. A different signature starts over.
+uint64_t fnv(uint64_t h, const void* p, size_t n) {
+    const unsigned char* b = static_cast<const unsigned char*>(p);
+    for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+    return h;
+}
+bool pool_order_on() {
+    static const bool on = [] {
+        const char* e = getenv("LRT_POOL_ORDER");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+int tile_order(KernelArgs& a, int kPix, long long ntiles, hipStream_t s, bool& record) {
+    record = false;
+    if (!pool_order_on() || ntiles < 2 * kV0Queues) return LRT_OK;
+    const int key[] = {a.width, a.height, a.x0, a.xc, a.y0, a.rows, a.rb, a.rp, a.rph, a.frames, a.maxDepth,
+                       a.ndl, a.bv.on, a.count, kPix, (int)g_ctx.scene_version, a.sph == g_ctx.d_sph ? 0 : 1};
+    uint64_t sig = fnv(1469598103934665603ull, key, sizeof(key));
+    sig = fnv(sig, &a.cam, sizeof(a.cam));
+    auto& o = g_ctx.order;
+    if (o.sig != sig || o.ntiles != ntiles) {   // a new signature: record its costs
+        // launches of the old signature (any stream) may still read its permutation or write
+        // its costs: let them finish before the buffers are reused
+        if (o.state != 0) LRT_HIP(hipDeviceSynchronize());
+        if (o.ntiles < ntiles) {
+            if (o.d_cost) (void)hipFree(o.d_cost);
+            if (o.d_perm) (void)hipFree(o.d_perm);
+            o.d_cost = nullptr;
+            o.d_perm = nullptr;
+            if (hipMalloc(&o.d_cost, sizeof(unsigned) * ntiles) != hipSuccess ||
+                hipMalloc(&o.d_perm, sizeof(int) * ntiles) != hipSuccess) {
+                o.state = 0;
+                o.ntiles = 0;
+                o.sig = 0;
+                return fail(LRT_E_NOMEM, "hipMalloc(tile order)");
+            }
+        }
+        if (!o.ev) LRT_HIP(hipEventCreateWithFlags(&o.ev, hipEventDisableTiming));
+        o.sig = sig;
+        o.ntiles = ntiles;
+        o.state = 1;
+        a.tcost = o.d_cost;
+        record = true;
+        return LRT_OK;
+    }
+    if (o.state == 1) {
+        hipError_t q = hipEventQuery(o.ev);
+        if (q == hipErrorNotReady) return LRT_OK;   // the recording launch is still running
+        if (q != hipSuccess) return hip_fail(q, "hipEventQuery(tile costs)");
+        std::vector<unsigned> cost((size_t)ntiles);
+        LRT_HIP(hipMemcpy(cost.data(), o.d_cost, sizeof(unsigned) * ntiles, hipMemcpyDeviceToHost));
+        o.h_perm.resize((size_t)ntiles);
+        for (long long i = 0; i < ntiles; ++i) o.h_perm[(size_t)i] = (int)i;
+        std::stable_sort(o.h_perm.begin(), o.h_perm.end(),
+                         [&](int x, int y) { return cost[(size_t)x] > cost[(size_t)y]; });
+        LRT_HIP(hipMemcpyAsync(o.d_perm, o.h_perm.data(), sizeof(int) * ntiles, hipMemcpyHostToDevice, s));
+        o.state = 2;
+    }
+    a.perm = o.d_perm;
+    return LRT_OK;
+}
+
 template <int MAXD, int kPix>
 int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     constexpr int TX = PoolTile<kPix>::X, TY = PoolTile<kPix>::Y;
@@ -1285,6 +1370,11 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     unsigned long long* d_sec = secstats_buffer(s);
     a.wtrace = d_sec;
 #endif
+#ifdef LRT_EXP_WAVETRACE
+    a.wtrace = wavetrace_buffer(grid.x);
+#endif
+    bool record = false;
+    if (int rc = tile_order(a, kPix, ntiles, s, record)) return rc;
     if (a.bv.on) {
         if (lds) pool_kernel<MAXD, true, true, kPix><<<grid, 64, ldsb, s>>>(a);
         else pool_kernel<MAXD, false, true, kPix><<<grid, 64, ldsb, s>>>(a);
@@ -1296,11 +1386,16 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     }
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "pool_kernel launch");
+    if (record) LRT_HIP(hipEventRecord(g_ctx.order.ev, s));
     snprintf(g_last_launch, sizeof(g_last_launch),
-             "kernel=pool_kernel maxd=%d lds=%d bvh=%d pix=%d ns=%d grid=%u tasks=%lld per_cu=%d", MAXD, lds ? 1 : 0,
-             a.bv.on ? 1 : 0, kPix, fixed ? kFixedSpheres : 0, grid.x, ntiles, per_cu);
+             "kernel=pool_kernel maxd=%d lds=%d bvh=%d pix=%d ns=%d grid=%u tasks=%lld order=%d per_cu=%d", MAXD,
+             lds ? 1 : 0, a.bv.on ? 1 : 0, kPix, fixed ? kFixedSpheres : 0, grid.x, ntiles,
+             a.perm ? 2 : record ? 1 : 0, per_cu);
 #ifdef LRT_EXP_SECSTATS
     secstats_dump(d_sec, s);
+#endif
+#ifdef LRT_EXP_WAVETRACE
+    wavetrace_dump(a.wtrace, grid.x, s);
 #endif
     e = hipFreeAsync(a.colbuf, s);
     if (e != hipSuccess) return hip_fail(e, "hipFreeAsync(pool colour slots)");
@@ -1493,6 +1588,8 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     a.lerp = g_ctx.d_lerp;
     a.colbuf = nullptr;
     a.poolSlots = 0;
+    a.perm = nullptr;
+    a.tcost = nullptr;
     a.samp = colours_out;
     a.sampOnly = colours_out ? 1 : 0;
     if (colours_out) {   // v0, one frame lane per pixel, sample mode
@@ -1522,13 +1619,15 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     return launch_split<64>(a, lds, d->x_count, d->row_count, d->frames, want_feat, s);
 }
 
-// The library's kernel policy (measured, profiles/r2_p2): the pool kernel (v5) where paths
-// are long or traversals expensive -- BVH scenes (config 4: 223 vs 303 ms, config 5) and
-// bounce budgets above 8 (config 3: 2.45 vs 2.87 ms) -- given at least 4 frames and two
-// tiles per resident wave; v0 otherwise (config 2: equal, 0.306 ms; few pixels with many
+// The library's kernel policy (measured, profiles/r2_p2, r2_p9): the pool kernel (v5) given
+// at least 4 frames and two tiles per resident wave -- BVH scenes (config 4: 223 vs 303
+// ms, config 5), bounce budgets above 8 (config 3: 2.45 vs 2.87 ms) and, with its
+// heaviest-first tile order (tile_order), the 8-bounce default scene too (config 2: 0.254 vs
+// 0.289 ms/step, 0.297 vs 0.329 ms for a launch alone); v0 otherwise (few pixels with many
 // frames, a GPU's row shard, take v0's frame lanes and sample mode; features are v0's).
 int auto_kernel(const KernelArgs& a, const lrt_render_desc* d, bool feat) {
-    if (feat || d->frames < 4 || !(a.bv.on || d->max_depth > 8)) return LRT_F_SIMPLE;
+    if (feat || d->frames < 4) return LRT_F_SIMPLE;
+    if (!(a.bv.on || d->max_depth > 8) && !pool_order_on()) return LRT_F_SIMPLE;
     int pix = 64;
     while (pix > 1 && pix * d->frames > kPoolSamples) pix /= (pix == 64 || pix == 32 ? 2 : 4);
     const int tx = pix >= 32 ? 8 : pix >= 8 ? 4 : pix >= 2 ? 2 : 1, ty = pix / tx;
@@ -1861,6 +1960,9 @@ int lrt_shutdown(void) {
         if (f) (void)hipFree(f);
     for (auto& m : g_ctx.masked_streams) (void)hipStreamDestroy(m.first);
     if (g_ctx.d_col) (void)hipFree(g_ctx.d_col);
+    if (g_ctx.order.d_cost) (void)hipFree(g_ctx.order.d_cost);
+    if (g_ctx.order.d_perm) (void)hipFree(g_ctx.order.d_perm);
+    if (g_ctx.order.ev) (void)hipEventDestroy(g_ctx.order.ev);
     for (int c = 0; c < Context::kHostChunks; ++c)
         if (g_ctx.ev_in[c]) (void)hipEventDestroy(g_ctx.ev_in[c]);
     if (g_ctx.s_in) (void)hipStreamDestroy(g_ctx.s_in);

@@ -92,6 +92,9 @@ __global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const Ker
         sc.sectime[1] = __builtin_amdgcn_s_memtime();
     }
 #endif
+#ifdef LRT_EXP_WAVETRACE
+    const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     float4* const lstk = smem + lane;   // this lane's recursion stack (LDS)
     const size_t gtid = (size_t)blockIdx.x * 64 + lane;
     const size_t gthreads = (size_t)gridDim.x * 64;
@@ -121,7 +124,9 @@ __global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const Ker
     const int nq = (ntiles - q + kV0Queues - 1) / kV0Queues;
     unsigned long long* ctr = a.tiles + q * kCtrStride;
     for (int i = blockIdx.x / kV0Queues; i < nq;) {
-        const int tile = q + kV0Queues * i;
+        const int task = q + kV0Queues * i;
+        const int tile = a.perm ? a.perm[task] : task;   // heaviest-first order (tile_order)
+        const unsigned long long tt0 = a.tcost ? __builtin_amdgcn_s_memrealtime() : 0ull;
         const int tx0 = (tile % tilesX) * TX, ty0 = (tile / tilesX) * TY;
         unsigned long long fetched = 0;
         if (lane == 0) fetched = atomicAdd(ctr, 1ull);   // consumed after the tile (hides its latency)
@@ -292,6 +297,7 @@ __global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const Ker
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         }
         if (mine) *mpx = acc;   // alpha as read
+        if (a.tcost && lane == 0) a.tcost[tile] = (unsigned)(__builtin_amdgcn_s_memrealtime() - tt0);
         const unsigned long long n = __shfl(fetched, 0, 64) + (unsigned long long)bq;
         i = n < (unsigned long long)nq ? (int)n : nq;
     }
@@ -304,6 +310,14 @@ __global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const Ker
             atomicAdd(g + 1, sc.sectime[2 + 2 * kSecN + k]);
             atomicAdd(g + 2, sc.sectime[2 + k]);
         }
+#endif
+#ifdef LRT_EXP_WAVETRACE
+    if (lane == 0) {
+        a.wtrace[4 * blockIdx.x + 0] = wt0;
+        a.wtrace[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+        a.wtrace[4 * blockIdx.x + 2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+        a.wtrace[4 * blockIdx.x + 3] = __builtin_amdgcn_s_getreg((15 << 11) | 20);   // XCC_ID
+    }
 #endif
     const unsigned long long total = wave_sum((unsigned long long)rays);
     if (lane == 0) block_epilogue(a.tiles, a.rays, q, bq, total);

@@ -119,3 +119,21 @@ def test_config5_shard_of_8_vs_oracle(gpu, scene1000, kflags):
         _bitwise(a[band * rb:(band + 1) * rb], want, f"config5 shard band {band}")
         rays += wr
     assert ra == rays
+
+
+@pytest.mark.parametrize("scene", ["config2_window", "scene1000"])
+def test_pool_tile_order_keeps_every_pixel(gpu, request, scene):
+    """The pool kernel's heaviest-first tile order (tile_order in lrt_hip.hip): the first
+    launch of a render signature records per-tile costs in queue order, the later ones hand
+    tiles out by descending cost. Every launch must give the same bits and ray count."""
+    kw = (dict(width=1280, height=720, frames=4, max_depth=8, x0=256, x_count=256, y0=128, row_count=128)
+          if scene == "config2_window" else
+          dict(width=3840, height=2160, frames=64, max_depth=8, x0=1800, x_count=64, y0=900, row_count=64))
+    if scene == "scene1000":
+        request.getfixturevalue("scene1000")
+    runs = [_render(gpu, flags=POOL, **kw) for _ in range(4)]
+    orders = [info.get("order") for _, _, info in runs]
+    assert orders[0] == "1" and orders[-1] == "2", orders   # recorded, then reordered
+    for k, (buf, rays, _) in enumerate(runs[1:], 1):
+        _bitwise(buf, runs[0][0], f"{scene} launch {k} vs the queue-order launch")
+        assert rays == runs[0][1]
