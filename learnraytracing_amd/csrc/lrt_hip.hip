@@ -8,6 +8,7 @@
 // of each pixel per call; rays counted per lane, reduced per wave, folded per queue.
 // Opt-in variants: v3 regeneration (lrt_regen.h), v4 wavefront (lrt_wavefront.h). Host side: scene upload + BVH build, launch policy, the C-ABI.
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include <math.h>
 #include <stdio.h>
 #include <string.h>
@@ -1905,6 +1906,13 @@ __global__ __launch_bounds__(64) void bvh_probe_kernel(BvhView bv, const float* 
 
 using namespace lrt;
 
+// roctx ranges around the C-ABI's work entry points (SURVEY §5 tracing): rocprofv3
+// --marker-trace shows each lrt_* call on the host timeline above the kernels it launched.
+struct RoctxRange {
+    explicit RoctxRange(const char* name) { roctxRangePushA(name); }
+    ~RoctxRange() { roctxRangePop(); }
+};
+
 extern "C" {
 
 const char* lrt_last_error(void) { return t_err.c_str(); }
@@ -1973,6 +1981,7 @@ int lrt_shutdown(void) {
 
 int lrt_draw_test(float time, int frameCount, int screenWidth, int screenHeight, float* backbuffer,
                   int* outRayCount) {
+    RoctxRange rr_("lrt_draw_test");
     (void)time;   // unused by the reference too (JobData::time, parallel.cpp:244)
     std::lock_guard<std::mutex> lk(g_mu);
     lrt_render_desc d;
@@ -2006,6 +2015,7 @@ int lrt_camera_make(lrt_float3 lookFrom, lrt_float3 lookAt, lrt_float3 vup, floa
 int lrt_camera_default(int width, int height, lrt_camera* out) { return camera_default(width, height, out); }
 
 int lrt_set_scene(const lrt_sphere* spheres, const lrt_material* materials, int count) {
+    RoctxRange rr_("lrt_set_scene");
     std::lock_guard<std::mutex> lk(g_mu);
     if (!g_ctx.ready) return fail(LRT_E_STATE, "lrt_initialize() has not been called");
     LRT_HIP(hipStreamSynchronize(g_ctx.stream));
@@ -2022,23 +2032,27 @@ int lrt_default_scene(lrt_sphere* spheres, lrt_material* materials, int capacity
 }
 
 int lrt_render_device(const lrt_render_desc* desc, float* d_backbuffer, unsigned long long* d_rays, void* stream) {
+    RoctxRange rr_("lrt_render_device");
     std::lock_guard<std::mutex> lk(g_mu);
     return render_device(desc, d_backbuffer, d_rays, nullptr, (hipStream_t)stream);
 }
 
 int lrt_render_device_ex(const lrt_render_desc* desc, float* d_backbuffer, unsigned long long* d_rays,
                          const lrt_features* d_features, void* stream) {
+    RoctxRange rr_("lrt_render_device_ex");
     std::lock_guard<std::mutex> lk(g_mu);
     return render_device(desc, d_backbuffer, d_rays, d_features, (hipStream_t)stream);
 }
 
 int lrt_render_host_ex(const lrt_render_desc* desc, float* backbuffer, long long* out_rays,
                        const lrt_features* features) {
+    RoctxRange rr_("lrt_render_host_ex");
     std::lock_guard<std::mutex> lk(g_mu);
     return render_host(desc, backbuffer, out_rays, features);
 }
 
 int lrt_render_host(const lrt_render_desc* desc, float* backbuffer, long long* out_rays) {
+    RoctxRange rr_("lrt_render_host");
     std::lock_guard<std::mutex> lk(g_mu);
     return render_host(desc, backbuffer, out_rays);
 }
@@ -2123,6 +2137,7 @@ int lrt_unshard_rows(const float* d_src, float* d_dst, int width, int height, in
 }
 
 int lrt_pack_rgb(const float* d_rgba, float* d_rgb, long long npix, void* stream) {
+    RoctxRange rr_("lrt_pack_rgb");
     if (!d_rgba || !d_rgb || npix < 0) return fail(LRT_E_INVALID, "invalid pack arguments");
     if (npix == 0) return LRT_OK;
     pack_rgb_kernel<<<(unsigned)((npix + 255) / 256), 256, 0, (hipStream_t)stream>>>(
@@ -2133,6 +2148,7 @@ int lrt_pack_rgb(const float* d_rgba, float* d_rgb, long long npix, void* stream
 
 int lrt_unshard_rows_rgb(const float* d_src_rgb, float* d_dst, int width, int height, int row_block, int period,
                          void* stream) {
+    RoctxRange rr_("lrt_unshard_rows_rgb");
     if (!d_src_rgb || !d_dst || width < 1 || height < 1 || row_block < 1 || period < 1)
         return fail(LRT_E_INVALID, "invalid unshard arguments");
     const int maxRows = lrt_shard_rows(height, row_block, period, 0);
@@ -2144,6 +2160,7 @@ int lrt_unshard_rows_rgb(const float* d_src_rgb, float* d_dst, int width, int he
 }
 
 int lrt_present_bgra8(const float* d_rgba, uint32_t* d_bgra, int width, int height, void* stream) {
+    RoctxRange rr_("lrt_present_bgra8");
     if (!d_rgba || !d_bgra || width < 1 || height < 1) return fail(LRT_E_INVALID, "invalid present arguments");
     int n = width * height;
     hipStream_t s = (hipStream_t)stream;

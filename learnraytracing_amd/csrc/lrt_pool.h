@@ -31,6 +31,9 @@ namespace lrt {
 #define LRT_POOL_SAMPLES 4096
 #endif
 constexpr int kPoolSamples = LRT_POOL_SAMPLES;
+#ifndef LRT_POOL_PACKET
+#define LRT_POOL_PACKET 0
+#endif
 enum : int { kPoolIdle = 0, kPoolTrace = 1, kPoolDone = 2, kPoolEnded = 3 };
 
 template <int kPix>
@@ -202,9 +205,12 @@ __global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const Ker
                     if (__ballot(state == kPoolIdle || state == kPoolEnded) == 0) break;   // the pool is dry
                     continue;
                 }
-                // camera rays that all start together (a round's first iteration) take the
-                // packet traversal (lrt_bvh.h)
-                const bool coherent = kBvh && LRT_PACKET_DEPTH > 0 && __ballot(state == kPoolTrace && depth != 0) == 0 &&
+                // LRT_POOL_PACKET: camera rays that all start together (a round's first
+                // iteration) take the packet traversal (lrt_bvh.h). Off: without the packet
+                // code the instance keeps its traversal state in fewer registers (config 4:
+                // 222.4 -> 209.8 ms/step, profiles/r2_q2)
+                const bool coherent = kBvh && LRT_POOL_PACKET && LRT_PACKET_DEPTH > 0 &&
+                                      __ballot(state == kPoolTrace && depth != 0) == 0 &&
                                       __ballot(state == kPoolTrace && pend) == 0;
                 sec_enter(sc, kSecOther, false);
                 // ---- one bounce of every traced path: Trace's body (parallel.cpp:202-226) ----

@@ -35,6 +35,21 @@ def test_library_is_gfx950_code():
     assert L.lib().lrt_version().decode().endswith("gfx950")
 
 
+def test_library_carries_roctx_ranges():
+    """SURVEY §5 tracing: the C-ABI's work entry points push roctx ranges (rocprofv3
+    --marker-trace), so the library imports the roctx API and names its ranges."""
+    import shutil
+    import subprocess
+    nm = shutil.which("nm")
+    if nm is None:
+        pytest.skip("nm not available")
+    und = subprocess.run([nm, "-D", "--undefined-only", L.LIB_PATH], capture_output=True, text=True).stdout
+    assert "roctxRangePushA" in und and "roctxRangePop" in und
+    blob = open(L.LIB_PATH, "rb").read()
+    for name in (b"lrt_draw_test", b"lrt_render_device", b"lrt_render_host", b"lrt_set_scene"):
+        assert name + b"\0" in blob
+
+
 def test_struct_layouts_match_reference():
     assert ctypes.sizeof(L.Float3) == 12          # maths.h float3
     assert ctypes.sizeof(L.Sphere) == 16          # maths.h Sphere
