@@ -133,11 +133,6 @@ __global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const Ker
         const int tx0 = (tile % tilesX) * TX, ty0 = (tile / tilesX) * TY;
         unsigned long long fetched = 0;
         if (lane == 0) fetched = atomicAdd(ctr, 1ull);   // consumed after the tile (hides its latency)
-        // lane j < kPix owns pixel j of the tile for the lerp chain and the store
-        const int mx = tx0 + lane % TX, my = ty0 + (lane / TX) % TY;
-        const bool mine = lane < kPix && mx < a.xc && my < a.rows;
-        float4* const mpx = a.out + (size_t)my * a.xc + mx;
-        float4 acc = mine ? *mpx : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         for (int fr0 = a.frame0; fr0 < fend; fr0 += kRoundFrames) {
             const int nfr = fend - fr0 < kRoundFrames ? fend - fr0 : kRoundFrames;
             const int N = nfr * kPix;   // this round's pool
@@ -283,10 +278,17 @@ __global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const Ker
                 }
             }
             // ---- the round's colours in frame order, one lane per pixel (:262,282) ---------
+            // Lane j < kPix owns pixel j of the tile. Its address and previous value are
+            // taken here, not held in registers through the bounce loop (fewer live VGPRs in
+            // the traversal); a later round re-reads what this one wrote.
             sec_enter(sc, kSecOther, false);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            const int mx = tx0 + lane % TX, my = ty0 + (lane / TX) % TY;
+            const bool mine = lane < kPix && mx < a.xc && my < a.rows;
             if (mine) {
+                float4* const mpx = a.out + (size_t)my * a.xc + mx;
+                float4 acc = *mpx;
                 F3 c3 = f3(acc.x, acc.y, acc.z);
                 for (int t = 0; t < nfr; ++t) {
                     const float4 c = slots[t * kPix + lane];
@@ -297,12 +299,12 @@ __global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const Ker
                 acc.x = c3.x;
                 acc.y = c3.y;
                 acc.z = c3.z;
+                *mpx = acc;   // alpha as read
             }
             // the next round overwrites the slots: every read above completes first
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         }
-        if (mine) *mpx = acc;   // alpha as read
         if (a.tcost && lane == 0) a.tcost[tile] = (unsigned)(__builtin_amdgcn_s_memrealtime() - tt0);
         const unsigned long long n = __shfl(fetched, 0, 64) + (unsigned long long)bq;
         i = n < (unsigned long long)nq ? (int)n : nq;
