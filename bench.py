@@ -125,6 +125,36 @@ def cpu_baseline(cfg, budget_s: float, cores: int):
                       f"{rays} rays in {dt:.2f} s, {cores} {'processes' if use_ref else 'threads'}; {src}"}
 
 
+def cpu_reference_drawtest(cores: int, budget_s: float):
+    """Context beside cpu_baseline: the reference as it ships -- its own
+    DrawTest (parallel.cpp:297-323) with enkiTS over `cores` workers, kMaxDepth 20 and the
+    shared racy RNG, at main.cpp's 1280x720, 1 spp per call, progressive frames on one
+    buffer. Not the same work as the metric (20 bounces, racy streams), so never a ratio."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure: the baseline legs only
+
+    if not oracle.have_ref(9):
+        return None
+    rate, frames, rays, dt = oracle.ref_drawtest_rate(1280, 720, budget_s, cores)
+    return {"value": round(rate, 3), "unit": "Mray/s", "cores": cores, "kind": "reference",
+            "sample": f"reference DrawTest (enkiTS, {cores} workers, kMaxDepth 20, shared RNG) at 1280x720, "
+                      f"{frames} progressive frame(s) x 1 spp, {rays} rays in {dt:.2f} s; oracle/_ref/libref.so"}
+
+
+def scene_reads(info: dict) -> str:
+    """Where the launched instance reads the scene from, taken from lrt_last_launch()'s
+    lds= / bvh= words (not from the flags asked for)."""
+    lds, bvh = info.get("lds"), info.get("bvh")
+    if bvh == "1":
+        return ("BVH nodes + leaf spheres through L1/L2 (global memory), materials "
+                + ("LDS-staged" if lds == "1" else "through L1/L2"))
+    if lds == "1":
+        return "LDS-staged spheres, materials and lights"
+    if lds == "0":
+        return "global memory (L1/L2)"
+    return "unknown"
+
+
 def read_pmc(key: str):
     """Per-launch counters of trace_kernel for `key` (e.g. "config2_n1") from the committed
     rocprofv3 passes (profiles/pmc_index.json -> profiles/<run>/summary_<config>.json)."""
@@ -163,8 +193,8 @@ def main():
     ap.add_argument("--scene-global", action="store_true", help="read spheres from global memory, not LDS")
     ap.add_argument("--reserve-cus", type=int, default=None,
                     help="CUs the render stream leaves free for other streams (default 0)")
-    ap.add_argument("--kernel", choices=["auto", "v0", "v3", "wf", "pool"], default="auto",
-                    help="auto: the library's policy; v0: frame lanes; v3: path regeneration; wf: wavefront; "
+    ap.add_argument("--kernel", choices=["auto", "v0", "wf", "pool"], default="auto",
+                    help="auto: the library's policy; v0: frame lanes; wf: wavefront; "
                          "pool: sample-pool regeneration (A/B)")
     args = ap.parse_args()
 
@@ -178,7 +208,7 @@ def main():
     extra = not args.no_extra_legs
 
     # CPU baselines first: rank 0 at N=1 only, before anything touches the GPU.
-    cpu = cpu1 = None
+    cpu = cpu1 = cpu_dt = None
     if rank == 0 and world == 1 and extra and not args.no_cpu_baseline:
         cores = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
         cores = max(1, min(cores, os.cpu_count() or 1))
@@ -187,6 +217,9 @@ def main():
         cpu = cpu_baseline(cfg, budget, cores)
         cpu1 = cpu_baseline(cfg, 6.0, 1)
         log(f"cpu baseline: {cpu['value']:.1f} Mray/s ({cpu['kind']}, {cores} cores), 1 core {cpu1['value']:.2f}")
+        cpu_dt = cpu_reference_drawtest(cores, 3.0)
+        if cpu_dt:
+            log(f"reference DrawTest (enkiTS, {cores} threads): {cpu_dt['value']:.1f} Mray/s")
 
     import torch
     import torch.distributed as dist
@@ -223,7 +256,7 @@ def main():
     rb = H if shards == 1 else args.row_block
     max_rows = max_shard_rows(H, rb, shards)
     rows = shard_rows(H, rb, shards, rank)
-    flags = (1 if args.scene_global else 0) | {"auto": 0, "v0": 2, "v3": 128, "wf": 256, "pool": 512}[args.kernel]
+    flags = (1 if args.scene_global else 0) | {"auto": 0, "v0": 2, "wf": 256, "pool": 512}[args.kernel]
     job = lrt.Job(width=W, height=H, frame0=0, frames=spp_total, max_depth=D, row_block=rb,
                   row_period=shards, row_phase=rank, row_count=rows, flags=flags)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -417,7 +450,7 @@ def main():
                 "parallelism": f"rows: row-block-cyclic x{world} (block {rb}), RCCL gather of RGB to rank 0"
                 if world > 1 else ("single GPU" if shards == 1 else
                                    f"DIAGNOSTIC: rank 0's shard of {shards} (block {rb}), no gather"),
-                "scene_reads": "global" if args.scene_global else "LDS-staged",
+                "scene_reads": scene_reads(launch_info),
                 "render_streams": nstreams,
                 "kernel": launch_info.get("kernel", args.kernel),
                 "instance": " ".join(f"{k}={v}" for k, v in launch_info.items() if k != "kernel"),
@@ -432,6 +465,7 @@ def main():
             } if e2e_s else None,
             "cpu_baseline": cpu,
             "cpu_baseline_1core": cpu1,
+            "cpu_reference_drawtest": cpu_dt,
         }
         print(json.dumps(out), flush=True)
     if rstream is not None:

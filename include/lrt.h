@@ -110,12 +110,10 @@ typedef struct lrt_render_desc {
                                 sampled explicitly); the terminating hit always adds it.
                                 Off by default: the CPU reference double counts
                                 (parallel.cpp:214). v0 kernel only.                   */
-#define LRT_F_V2 16          /* removed, as LRT_F_V1. With none of SIMPLE/V3/WAVEFRONT
-                                set the library runs SIMPLE (fastest on every config). */
-#define LRT_F_V3 128         /* v3 kernel: the v0 loop with path regeneration inside the
-                                wave (a lane traces its pixel's frames in turn; ended
-                                lanes are refilled together from the wave's pixel
-                                stream). No lrt_features.                              */
+#define LRT_F_V2 16          /* removed, as LRT_F_V1. With none of SIMPLE/WAVEFRONT/POOL
+                                set the library picks v0 or v5 per call (auto_kernel). */
+#define LRT_F_V3 128         /* removed in round 3 (round-1 path regeneration per pixel
+                                group: slower than v0 or v5 on every config), as LRT_F_V1 */
 #define LRT_F_WAVEFRONT 256  /* v4: wavefront (breadth-first) path tracing: path state in
                                 HBM, closest-hit and per-material shading kernels over
                                 compacted queues, frame planes merged in order. No
@@ -141,6 +139,24 @@ int lrt_shutdown(void);
  * `time` is accepted and unused, as in the reference. */
 int lrt_draw_test(float time, int frameCount, int screenWidth, int screenHeight,
                   float* backbuffer, int* outRayCount);
+
+/* ---- multi-GPU (one process) ---------------------------------------------- */
+
+/* InitializeTest over several devices (BASELINE config 5: the frame row-tiled across the
+ * node's GPUs, assembled by an RCCL gather over xGMI). Instead of lrt_initialize: n device
+ * ids (n = 0 and device_ids = NULL: every visible device). Afterwards lrt_draw_test and
+ * lrt_render_host(_ex without features) split the caller's rows over all of them in blocks of
+ * 8 rows dealt round-robin (row-block-cyclic; LRT_ROW_BLOCK overrides), each device renders its
+ * rows with the previous values copied from the caller's buffer, and the shards are gathered
+ * into the first device -- ncclCommInitAll + a grouped ncclGather (RCCL) when the ids are
+ * distinct, device-to-device copies when an id repeats (RCCL refuses two ranks on one GPU) or
+ * with LRT_DEV_PEER_COPY -- which assembles the frame and copies it to the caller. The result
+ * is bit-identical to one device. The other calls (lrt_render_device, streams, scene) act on
+ * the first device; lrt_set_scene updates every device. lrt_shutdown releases all. */
+#define LRT_DEV_PEER_COPY 1 /* gather with device-to-device copies instead of RCCL */
+int lrt_initialize_devices(int n, const int* device_ids, int flags);
+/* Devices in use (0 before lrt_initialize / lrt_initialize_devices). */
+int lrt_device_count(void);
 
 /* ---- extended API -------------------------------------------------------- */
 
@@ -216,6 +232,13 @@ int lrt_stream_destroy(void* stream);
  * (LRT_HOST_ZEROCOPY=0 turns that off). Free with lrt_host_free. */
 int lrt_host_alloc(size_t bytes, void** out);
 int lrt_host_free(void* p);
+/* A PAGEABLE host backbuffer (the reference's `new float[]`, main.cpp:40) that lrt_draw_test
+ * sees on two consecutive calls is page-locked in place (hipHostRegister) and from then on
+ * takes the page-locked paths; up to 8 such buffers stay registered. The caller must call
+ * lrt_host_unregister(buf) before freeing such a buffer while the library is initialised
+ * (lrt_shutdown unregisters every one); the reference's caller keeps its buffer for the whole
+ * run. lrt_render_host never registers. LRT_HOST_REGISTER=0 keeps pageable buffers staged. */
+int lrt_host_unregister(void* p);
 
 /* Number of local rows GPU `phase` owns in a row-block-cyclic split of `height` rows
  * into blocks of row_block rows dealt over `period` GPUs. */

@@ -31,8 +31,10 @@ F_V2S = 8
 F_V2 = 16
 F_NO_BVH = 32
 F_NO_DOUBLE_LIGHT = 64
-F_V3 = 128
+F_V3 = 128          # removed in round 3: rejected with LRT_E_INVALID
 F_WAVEFRONT = 256
+F_POOL = 512
+DEV_PEER_COPY = 1   # lrt_initialize_devices: gather by device-to-device copies, not RCCL
 
 
 class LrtError(RuntimeError):
@@ -98,6 +100,9 @@ SIGNATURES = {
     "lrt_draw_test": (_i, [_c.c_float, _i, _i, _i, _vp, _c.POINTER(_i)]),
     "lrt_last_error": (_c.c_char_p, []),
     "lrt_version": (_c.c_char_p, []),
+    "lrt_initialize_devices": (_i, [_i, _vp, _i]),
+    "lrt_device_count": (_i, []),
+    "lrt_host_unregister": (_i, [_vp]),
     "lrt_last_launch": (_c.c_char_p, []),
     "lrt_camera_make": (_i, [Float3, Float3, Float3, _c.c_float, _c.c_float, _c.c_float,
                              _c.c_float, _c.POINTER(Camera)]),
@@ -151,7 +156,11 @@ def lib() -> ctypes.CDLL:
             except OSError as e:   # pragma: no cover - depends on the box
                 raise LrtError(LRT_E_STATE, f"cannot load {LIB_PATH}: {e}") from e
             for name, (res, args) in SIGNATURES.items():
-                fn = getattr(handle, name)
+                fn = getattr(handle, name, None)
+                if fn is None and os.environ.get("LRT_LIB"):
+                    continue   # an A/B build of an older revision: entry points it predates stay unbound
+                if fn is None:
+                    raise LrtError(LRT_E_STATE, f"{LIB_PATH} does not export {name}")
                 fn.restype = res
                 fn.argtypes = args
             _lib = handle

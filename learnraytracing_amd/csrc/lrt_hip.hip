@@ -6,9 +6,17 @@
 // buffer's prev value); persistent single-wave workgroups fed from 16 tile queues; the
 // scene, the powf tables and the recursion stack in LDS; one read and one 16-byte write
 // of each pixel per call; rays counted per lane, reduced per wave, folded per queue.
-// Opt-in variants: v3 regeneration (lrt_regen.h), v4 wavefront (lrt_wavefront.h). Host side: scene upload + BVH build, launch policy, the C-ABI.
+// v5 (pool_kernel, lrt_pool.h) adds sample-pool regeneration; v4 wavefront (lrt_wavefront.h)
+// is opt-in. Host side: scene upload + BVH build, launch policy, multi-device split with the
+// RCCL gather, the C-ABI.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#ifndef LRT_ROCTX   // roctx ranges (tracing only): the Makefile sets it when the header exists
+#define LRT_ROCTX 0
+#endif
+#if LRT_ROCTX
 #include <rocprofiler-sdk-roctx/roctx.h>
+#endif
 #include <math.h>
 #include <stdio.h>
 #include <string.h>
@@ -79,7 +87,7 @@ struct KernelArgs {
     // world_pos_std (any may be null) and the last frame they are updated for (< 0: all)
     float4* feat[6];
     int featMax;
-    int regenMin;                 // v3: ended lanes that trigger a regeneration round
+    int regenMin;                 // v5: waiting lanes that trigger a refill
     const float* lerp;            // lerpFac = (float)f / (float)(f + 1) for f < kLerpTable (parallel.cpp:262)
     float4* samp;                 // sample mode: frames planes of xc * rows colours
     float4* colbuf;               // v5 (pool): poolSlots colour slots per block
@@ -369,7 +377,6 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
 }
 
 }  // namespace lrt
-#include "lrt_regen.h"
 #include "lrt_pool.h"
 namespace lrt {
 // (lrt_wavefront.h follows merge_samples_kernel)
@@ -508,17 +515,25 @@ struct Context {
     } wf;
     unsigned tiles_next = 0;
     unsigned scene_version = 0;   // bumped by every scene upload (tile-order signatures)
-    // The pool kernel's tile order for the last render signature seen (tile_order()):
-    // per-tile costs recorded by one launch, then a heaviest-first permutation for the rest.
+    // The pool kernel's tile orders, one per recent render signature (tile_order()): per-tile
+    // costs recorded by one launch, then a heaviest-first permutation for the later ones.
     struct TileOrder {
-        uint64_t sig = 0;
-        long long ntiles = 0;
-        int state = 0;                 // 0: none, 1: costs being recorded, 2: permutation ready
+        uint64_t sig = 0;              // the render signature (geometry, camera, scene)
+        uint64_t gkey = 0;             // its geometry only: views that can share an order
+        long long ntiles = 0, cap = 0;
+        int state = 0;                 // 0: free, 1: costs being recorded, 2: permutation ready
         unsigned* d_cost = nullptr;
-        int* d_perm = nullptr;
-        hipEvent_t ev = nullptr;       // the recording launch's end
-        std::vector<int> h_perm;       // the upload's source (kept alive)
-    } order;
+        int* d_perm = nullptr;         // written once (state 1 -> 2), read by every later launch
+        hipEvent_t ev_rec = nullptr;   // the recording launch's end
+        int donor = -1;                // state 1: the entry whose ready order launches borrow meanwhile
+        // the streams whose launches read d_perm / wrote d_cost, each with an event after its
+        // last such launch: the entry is reused only once all of them have passed it
+        std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
+        unsigned long long tick = 0;   // least recently used goes first
+    };
+    static constexpr int kOrderSlots = 8;
+    TileOrder order[kOrderSlots];
+    unsigned long long order_tick = 0;
     hipStream_t stream = nullptr;
     int count = 0, nlights = 0;
     float4* d_sph = nullptr;
@@ -545,12 +560,36 @@ struct Context {
     size_t feat_bytes[6] = {};
     size_t frame_bytes = 0;
     unsigned long long* d_rays = nullptr;
+    // multi-device renders (lrt_initialize_devices): this device's row shard, packed for
+    // the exchange, and (device 0) the gathered shards
+    float* d_shard = nullptr;
+    size_t shard_bytes = 0;
+    float* d_gath = nullptr;
+    size_t gath_bytes = 0;
+    hipEvent_t ev_done = nullptr;   // this device's part of a multi-device render is enqueued
 };
 
-Context g_ctx;
+// One context per device in use: lrt_initialize binds the caller's current device (context
+// 0); lrt_initialize_devices binds a list, and host renders are split over all of them.
+constexpr int kMaxDevices = 16;
+Context g_devs[kMaxDevices];
+int g_ndev = 0;   // contexts in use
+int g_cur = 0;    // the context the functions below act on (set under g_mu)
+Context& ctx() { return g_devs[g_cur]; }
+
+// Multi-device state (lrt_initialize_devices).
+struct Multi {
+    bool on = false;          // host renders are split over the g_ndev contexts
+    bool rccl = false;        // the shards are gathered by RCCL (distinct devices); else peer copies
+    int row_block = 8;        // rows per block of the row-block-cyclic split (LRT_ROW_BLOCK)
+    ncclComm_t comms[kMaxDevices] = {};
+};
+Multi g_multi;
+
 std::mutex g_mu;
 char g_last_launch[256] = "";   // lrt_last_launch(): the kernel instance of the last render call
 thread_local std::string t_err;
+thread_local std::string t_launch;   // lrt_last_launch()'s copy for the calling thread
 
 int fail(int code, const std::string& msg) {
     t_err = msg;
@@ -1036,7 +1075,7 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     a.bvh_stack_offset = (int)(stack + scene);
     // v0 sizes the LDS traversal stack to this scene's BVH depth (1000 spheres: ~9
     // levels, 1.2 KB instead of 3 KB per wave -- the difference between 13 and 16 waves/CU)
-    const size_t bstk = a.bv.on ? sizeof(unsigned short) * g_ctx.bvh_stack_levels * kBlock : 0;
+    const size_t bstk = a.bv.on ? sizeof(unsigned short) * ctx().bvh_stack_levels * kBlock : 0;
     const size_t ldsb = stack + (lds ? scene : 0) + bstk;
     // the reference's own scene size (parallel.cpp:27) gets the unrolled-scan instances
     const bool fixed = lds && !a.bv.on && a.count == kFixedSpheres;
@@ -1051,8 +1090,8 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     if (per_cu < 1) return fail(LRT_E_INVALID, "trace_kernel does not fit on a CU");
     // a CU-masked render stream (lrt_stream_create) gets a grid for the CUs it may use:
     // persistent blocks beyond those would only start when others finish
-    int cus = g_ctx.num_cus;
-    for (const auto& m : g_ctx.masked_streams)
+    int cus = ctx().num_cus;
+    for (const auto& m : ctx().masked_streams)
         if (m.first == s) cus = m.second;
     // Sample mode (kSamp): several rounds per pixel and fewer than 16 tasks per resident
     // wave (a row shard of a multi-GPU frame at N x spp) -- one task per (tile, round)
@@ -1082,7 +1121,7 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     const dim3 grid((unsigned)blocks);
     if (!a.sampOnly) a.samp = nullptr;
     a.ovf = nullptr;
-    a.tiles = g_ctx.d_tiles + (size_t)(g_ctx.tiles_next++ % kQueueSlots) * kTileSetU64;
+    a.tiles = ctx().d_tiles + (size_t)(ctx().tiles_next++ % kQueueSlots) * kTileSetU64;
 #ifdef LRT_EXP_SECSTATS
     unsigned long long* d_sec = secstats_buffer(s);
     a.wtrace = d_sec;
@@ -1177,77 +1216,6 @@ int launch_split(const KernelArgs& a, bool lds, int xc, int rows, int frames, bo
     }
 }
 
-// v3 (lrt_regen.h): same LDS layout, queues, counters and overflow stack as v0.
-template <int MAXD, int kSplit>
-int launch_regen(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
-    constexpr int kTileRows = 8 / kSplit;
-    const long long ntiles = (long long)((xc + 7) / 8) * ((rows + kTileRows - 1) / kTileRows);
-    const size_t stack = sizeof(float4) * kTraceLdsLevels * 64 + kPowTableBytes + kRenormBytes;
-    const size_t scene = lds ? sizeof(float4) * (4 * (size_t)a.count + (size_t)(a.nlights + 3) / 4 + 1) : 0;
-    a.bvh_stack_offset = (int)(stack + scene);
-    const size_t bstk = a.bv.on ? sizeof(unsigned short) * g_ctx.bvh_stack_levels * 64 : 0;
-    const size_t ldsb = stack + scene + bstk;
-    const void* kern = a.bv.on ? (lds ? (const void*)regen_kernel<MAXD, true, true, kSplit> : (const void*)regen_kernel<MAXD, false, true, kSplit>)
-                               : (lds ? (const void*)regen_kernel<MAXD, true, false, kSplit> : (const void*)regen_kernel<MAXD, false, false, kSplit>);
-    int per_cu = 0;
-    hipError_t e = occupancy(&per_cu, kern, 64, ldsb);
-    if (e != hipSuccess) return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
-    if (per_cu < 1) return fail(LRT_E_INVALID, "regen_kernel does not fit on a CU");
-    int cus = g_ctx.num_cus;
-    for (const auto& m : g_ctx.masked_streams)
-        if (m.first == s) cus = m.second;
-    long long blocks = std::max((long long)per_cu * cus, (long long)kV0Queues);   // a block per queue (as v0)
-    if (blocks > ntiles) blocks = ntiles;
-    const dim3 grid((unsigned)blocks);
-    a.ovf = nullptr;
-    a.tiles = g_ctx.d_tiles + (size_t)(g_ctx.tiles_next++ % kQueueSlots) * kTileSetU64;
-    if (a.regenMin <= 0) {
-        static int env = -1;
-        if (env < 0) {
-            const char* v = getenv("LRT_V3_REGEN_MIN");
-            env = v ? atoi(v) : 0;
-            if (env <= 0 || env > 64) env = 16;
-        }
-        a.regenMin = env;
-    }
-    if (a.maxDepth > kTraceLdsLevels) {
-        const size_t gthreads = (size_t)grid.x * 64;
-        e = hipMallocAsync((void**)&a.ovf, sizeof(float4) * gthreads * (size_t)(a.maxDepth - kTraceLdsLevels), s);
-        if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(trace stack overflow)");
-    }
-#ifdef LRT_EXP_SECSTATS
-    unsigned long long* d_sec = secstats_buffer(s);
-    a.wtrace = d_sec;
-#endif
-    if (a.bv.on) {
-        if (lds) regen_kernel<MAXD, true, true, kSplit><<<grid, 64, ldsb, s>>>(a);
-        else regen_kernel<MAXD, false, true, kSplit><<<grid, 64, ldsb, s>>>(a);
-    } else {
-        if (lds) regen_kernel<MAXD, true, false, kSplit><<<grid, 64, ldsb, s>>>(a);
-        else regen_kernel<MAXD, false, false, kSplit><<<grid, 64, ldsb, s>>>(a);
-    }
-    e = hipGetLastError();
-    if (e != hipSuccess) return hip_fail(e, "regen_kernel launch");
-    snprintf(g_last_launch, sizeof(g_last_launch), "kernel=regen_kernel maxd=%d lds=%d bvh=%d split=%d grid=%u tasks=%lld",
-             MAXD, lds ? 1 : 0, a.bv.on ? 1 : 0, kSplit, grid.x, ntiles);
-
-#ifdef LRT_EXP_SECSTATS
-    secstats_dump(d_sec, s);
-#endif
-    if (a.ovf) {
-        e = hipFreeAsync(a.ovf, s);
-        if (e != hipSuccess) return hip_fail(e, "hipFreeAsync(trace stack overflow)");
-    }
-    return LRT_OK;
-}
-
-template <int MAXD>
-int launch_regen_split(const KernelArgs& a, bool lds, int xc, int rows, int frames, hipStream_t s) {
-    if (frames >= 4) return launch_regen<MAXD, 4>(a, lds, xc, rows, s);
-    if (frames >= 2) return launch_regen<MAXD, 2>(a, lds, xc, rows, s);
-    return launch_regen<MAXD, 1>(a, lds, xc, rows, s);
-}
-
 // v5 (lrt_pool.h): v0's LDS layout, queues, counters and overflow stack, plus the
 // per-block colour slots.
 // Heaviest-first tile order for the pool kernel (LRT_POOL_ORDER=0: off). A pool tile is
@@ -1257,7 +1225,12 @@ int launch_regen_split(const KernelArgs& a, bool lds, int xc, int rows, int fram
 // camera, scene, tile size) records each tile's cost; once it has finished, the next launch
 // of that signature sorts the costs on the host and hands tiles out heaviest first -- the
 // classic LPT order -- and so does every later one. Each pixel's result is unchanged: only
-// the order in which tiles are taken changes. A different signature starts over.
+// the order in which tiles are taken changes.
+// The last kOrderSlots signatures keep their orders, so callers alternating renders (two
+// windows, a DrawTest beside a device render) neither start over nor wait. A new view of the
+// same geometry (the camera moved, the scene was edited) borrows the newest ready order of
+// that geometry for its own recording launch and until its costs are in: its first launch
+// already runs heaviest-first by the previous view's measure.
 uint64_t fnv(uint64_t h, const void* p, size_t n) {
     const unsigned char* b = static_cast<const unsigned char*>(p);
     for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
@@ -1270,53 +1243,106 @@ bool pool_order_on() {
     }();
     return on;
 }
-int tile_order(KernelArgs& a, int kPix, long long ntiles, hipStream_t s, bool& record) {
-    record = false;
-    if (!pool_order_on() || ntiles < 2 * kV0Queues) return LRT_OK;
-    const int key[] = {a.width, a.height, a.x0, a.xc, a.y0, a.rows, a.rb, a.rp, a.rph, a.frames, a.maxDepth,
-                       a.ndl, a.bv.on, a.count, kPix, (int)g_ctx.scene_version, a.sph == g_ctx.d_sph ? 0 : 1};
-    uint64_t sig = fnv(1469598103934665603ull, key, sizeof(key));
-    sig = fnv(sig, &a.cam, sizeof(a.cam));
-    auto& o = g_ctx.order;
-    if (o.sig != sig || o.ntiles != ntiles) {   // a new signature: record its costs
-        // launches of the old signature (any stream) may still read its permutation or write
-        // its costs: let them finish before the buffers are reused
-        if (o.state != 0) LRT_HIP(hipDeviceSynchronize());
-        if (o.ntiles < ntiles) {
-            if (o.d_cost) (void)hipFree(o.d_cost);
-            if (o.d_perm) (void)hipFree(o.d_perm);
-            o.d_cost = nullptr;
-            o.d_perm = nullptr;
-            if (hipMalloc(&o.d_cost, sizeof(unsigned) * ntiles) != hipSuccess ||
-                hipMalloc(&o.d_perm, sizeof(int) * ntiles) != hipSuccess) {
-                o.state = 0;
-                o.ntiles = 0;
-                o.sig = 0;
-                return fail(LRT_E_NOMEM, "hipMalloc(tile order)");
-            }
+// Waits until every launch that used entry e has passed it (only those streams' events).
+int order_release(Context::TileOrder& e) {
+    for (auto& u : e.uses) LRT_HIP(hipEventSynchronize(u.second));
+    return LRT_OK;
+}
+// After a launch on stream s that read e's permutation or wrote its costs.
+int order_used(Context::TileOrder& e, hipStream_t s) {
+    for (auto& u : e.uses)
+        if (u.first == s) {
+            LRT_HIP(hipEventRecord(u.second, s));
+            return LRT_OK;
         }
-        if (!o.ev) LRT_HIP(hipEventCreateWithFlags(&o.ev, hipEventDisableTiming));
-        o.sig = sig;
-        o.ntiles = ntiles;
-        o.state = 1;
-        a.tcost = o.d_cost;
+    hipEvent_t ev = nullptr;
+    LRT_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    e.uses.emplace_back(s, ev);
+    LRT_HIP(hipEventRecord(ev, s));
+    return LRT_OK;
+}
+// Picks a's order for this launch: a.perm (null: queue order) and, for the recording launch,
+// a.tcost. *users gets the entries whose buffers the launch touches (order_used after it).
+int tile_order(KernelArgs& a, int kPix, long long ntiles, bool& record, Context::TileOrder* users[2]) {
+    record = false;
+    users[0] = users[1] = nullptr;
+    if (!pool_order_on() || ntiles < 2 * kV0Queues) return LRT_OK;
+    Context& c = ctx();
+    const int geo[] = {a.width, a.height, a.x0, a.xc, a.y0, a.rows, a.rb, a.rp, a.rph, a.frames, a.maxDepth,
+                       a.ndl, a.bv.on, a.count, kPix, a.sph == c.d_sph ? 0 : 1};
+    const uint64_t gkey = fnv(1469598103934665603ull, geo, sizeof(geo));
+    uint64_t sig = fnv(gkey, &c.scene_version, sizeof(c.scene_version));
+    sig = fnv(sig, &a.cam, sizeof(a.cam));
+    Context::TileOrder* e = nullptr;
+    for (auto& o : c.order)
+        if (o.state != 0 && o.sig == sig && o.ntiles == ntiles) e = &o;
+    if (!e) {   // a new signature: take a free entry, else the least recently used one
+        for (auto& o : c.order)
+            if (!e && o.state == 0) e = &o;
+        if (!e) {
+            e = &c.order[0];
+            for (auto& o : c.order)
+                if (o.tick < e->tick) e = &o;
+        }
+        int donor = -1;   // the newest ready order of the same geometry
+        for (int i = 0; i < Context::kOrderSlots; ++i) {
+            const auto& o = c.order[i];
+            if (&o != e && o.state == 2 && o.gkey == gkey && o.ntiles == ntiles &&
+                (donor < 0 || o.tick > c.order[donor].tick))
+                donor = i;
+        }
+        if (e->state != 0) {
+            // launches that read this entry's permutation (also as a donor) must be done
+            // with it; the entries borrowing it lose their donor
+            if (int rc = order_release(*e)) return rc;
+            for (auto& o : c.order)
+                if (o.donor == (int)(e - c.order)) o.donor = -1;
+        }
+        if (e->cap < ntiles) {
+            if (e->d_cost) (void)hipFree(e->d_cost);
+            if (e->d_perm) (void)hipFree(e->d_perm);
+            e->d_cost = nullptr;
+            e->d_perm = nullptr;
+            e->cap = 0;
+            e->state = 0;
+            if (hipMalloc(&e->d_cost, sizeof(unsigned) * ntiles) != hipSuccess ||
+                hipMalloc(&e->d_perm, sizeof(int) * ntiles) != hipSuccess)
+                return fail(LRT_E_NOMEM, "hipMalloc(tile order)");
+            e->cap = ntiles;
+        }
+        if (!e->ev_rec) LRT_HIP(hipEventCreateWithFlags(&e->ev_rec, hipEventDisableTiming));
+        e->sig = sig;
+        e->gkey = gkey;
+        e->ntiles = ntiles;
+        e->state = 1;
+        e->donor = donor;
+        a.tcost = e->d_cost;
         record = true;
-        return LRT_OK;
+    } else if (e->state == 1) {
+        const hipError_t q = hipEventQuery(e->ev_rec);
+        if (q != hipSuccess && q != hipErrorNotReady) return hip_fail(q, "hipEventQuery(tile costs)");
+        if (q == hipSuccess) {   // the costs are in: sort them (once per signature)
+            std::vector<unsigned> cost((size_t)ntiles);
+            LRT_HIP(hipMemcpy(cost.data(), e->d_cost, sizeof(unsigned) * ntiles, hipMemcpyDeviceToHost));
+            std::vector<int> perm((size_t)ntiles);
+            for (long long i = 0; i < ntiles; ++i) perm[(size_t)i] = (int)i;
+            std::stable_sort(perm.begin(), perm.end(), [&](int x, int y) { return cost[(size_t)x] > cost[(size_t)y]; });
+            // blocking: the permutation is in device memory before ANY stream's launch reads
+            // it (no launch has read this entry's d_perm yet)
+            LRT_HIP(hipMemcpy(e->d_perm, perm.data(), sizeof(int) * ntiles, hipMemcpyHostToDevice));
+            e->state = 2;
+            e->donor = -1;
+        }
     }
-    if (o.state == 1) {
-        hipError_t q = hipEventQuery(o.ev);
-        if (q == hipErrorNotReady) return LRT_OK;   // the recording launch is still running
-        if (q != hipSuccess) return hip_fail(q, "hipEventQuery(tile costs)");
-        std::vector<unsigned> cost((size_t)ntiles);
-        LRT_HIP(hipMemcpy(cost.data(), o.d_cost, sizeof(unsigned) * ntiles, hipMemcpyDeviceToHost));
-        o.h_perm.resize((size_t)ntiles);
-        for (long long i = 0; i < ntiles; ++i) o.h_perm[(size_t)i] = (int)i;
-        std::stable_sort(o.h_perm.begin(), o.h_perm.end(),
-                         [&](int x, int y) { return cost[(size_t)x] > cost[(size_t)y]; });
-        LRT_HIP(hipMemcpyAsync(o.d_perm, o.h_perm.data(), sizeof(int) * ntiles, hipMemcpyHostToDevice, s));
-        o.state = 2;
+    if (e->state == 2) {
+        a.perm = e->d_perm;
+    } else if (e->donor >= 0) {
+        users[1] = &c.order[e->donor];
+        a.perm = users[1]->d_perm;
+        users[1]->tick = ++c.order_tick;
     }
-    a.perm = o.d_perm;
+    users[0] = e;
+    e->tick = ++c.order_tick;
     return LRT_OK;
 }
 
@@ -1327,7 +1353,7 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     const size_t stack = sizeof(float4) * kTraceLdsLevels * 64 + kPowTableBytes + (a.bv.on ? 0 : kRenormBytes);
     const size_t scene = lds ? sizeof(float4) * (4 * (size_t)a.count + (size_t)(a.nlights + 3) / 4 + 1) : 0;
     a.bvh_stack_offset = (int)(stack + scene);
-    const size_t bstk = a.bv.on ? sizeof(unsigned short) * g_ctx.bvh_stack_levels * 64 : 0;
+    const size_t bstk = a.bv.on ? sizeof(unsigned short) * ctx().bvh_stack_levels * 64 : 0;
     const size_t ldsb = stack + scene + bstk;
     const bool fixed = lds && !a.bv.on && a.count == kFixedSpheres;
     const void* kern = a.bv.on ? (lds ? (const void*)pool_kernel<MAXD, true, true, kPix>
@@ -1339,15 +1365,15 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     hipError_t e = occupancy(&per_cu, kern, 64, ldsb);
     if (e != hipSuccess) return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
     if (per_cu < 1) return fail(LRT_E_INVALID, "pool_kernel does not fit on a CU");
-    int cus = g_ctx.num_cus;
-    for (const auto& m : g_ctx.masked_streams)
+    int cus = ctx().num_cus;
+    for (const auto& m : ctx().masked_streams)
         if (m.first == s) cus = m.second;
     long long blocks = std::max((long long)per_cu * cus, (long long)kV0Queues);   // a block per queue (as v0)
     if (blocks > ntiles) blocks = ntiles;
     const dim3 grid((unsigned)blocks);
     a.ovf = nullptr;
     a.colbuf = nullptr;
-    a.tiles = g_ctx.d_tiles + (size_t)(g_ctx.tiles_next++ % kQueueSlots) * kTileSetU64;
+    a.tiles = ctx().d_tiles + (size_t)(ctx().tiles_next++ % kQueueSlots) * kTileSetU64;
     {   // waiting lanes that trigger a refill (fold + next samples); LRT_POOL_REFILL_MIN.
         // Measured (profiles/r2_p2): config 3 2.31 -> 2.05 ms/step at 16 (vs 1), config 4 and
         // config 2 neutral
@@ -1375,7 +1401,8 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     a.wtrace = wavetrace_buffer(grid.x);
 #endif
     bool record = false;
-    if (int rc = tile_order(a, kPix, ntiles, s, record)) return rc;
+    Context::TileOrder* users[2];
+    if (int rc = tile_order(a, kPix, ntiles, record, users)) return rc;
     if (a.bv.on) {
         if (lds) pool_kernel<MAXD, true, true, kPix><<<grid, 64, ldsb, s>>>(a);
         else pool_kernel<MAXD, false, true, kPix><<<grid, 64, ldsb, s>>>(a);
@@ -1387,11 +1414,14 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     }
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "pool_kernel launch");
-    if (record) LRT_HIP(hipEventRecord(g_ctx.order.ev, s));
+    if (record) LRT_HIP(hipEventRecord(users[0]->ev_rec, s));
+    for (auto* u : users)
+        if (u)
+            if (int rc = order_used(*u, s)) return rc;
     snprintf(g_last_launch, sizeof(g_last_launch),
              "kernel=pool_kernel maxd=%d lds=%d bvh=%d pix=%d ns=%d grid=%u tasks=%lld order=%d per_cu=%d", MAXD,
              lds ? 1 : 0, a.bv.on ? 1 : 0, kPix, fixed ? kFixedSpheres : 0, grid.x, ntiles,
-             a.perm ? 2 : record ? 1 : 0, per_cu);
+             users[0] && users[0]->state == 2 ? 2 : users[1] ? 3 : record ? 1 : 0, per_cu);
 #ifdef LRT_EXP_SECSTATS
     secstats_dump(d_sec, s);
 #endif
@@ -1436,7 +1466,7 @@ int launch_wavefront(KernelArgs a, bool lds, hipStream_t s) {
     // the persistent grid: every wavefront kernel runs B blocks, block j on region j
     const size_t head = kPowTableBytes + kRenormBytes;
     const size_t scene = lds ? sizeof(float4) * (4 * (size_t)a.count + (size_t)(a.nlights + 3) / 4 + 1) : 0;
-    const size_t bstk = a.bv.on ? sizeof(unsigned short) * g_ctx.bvh_stack_levels * kWfBlock : 0;
+    const size_t bstk = a.bv.on ? sizeof(unsigned short) * ctx().bvh_stack_levels * kWfBlock : 0;
     const size_t ldsb = head + scene + bstk;
     const bool bvh = a.bv.on != 0, fixed = lds && !bvh && a.count == kFixedSpheres;
     const void* kx = bvh ? (const void*)wf_extend<true, 0> : fixed ? (const void*)wf_extend<false, kFixedSpheres>
@@ -1449,10 +1479,10 @@ int launch_wavefront(KernelArgs a, bool lds, hipStream_t s) {
     if (e != hipSuccess) return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
     per_cu = std::min(per_cu, per_cu_s);
     if (per_cu < 1) return fail(LRT_E_INVALID, "wavefront kernels do not fit on a CU");
-    const int B = per_cu * g_ctx.num_cus;
+    const int B = per_cu * ctx().num_cus;
     const size_t cnt_bytes = sizeof(unsigned int) * 4 * (size_t)(a.maxDepth + 2) * B;
     const size_t need = per_path * (C + (size_t)B) + cnt_bytes + 256 * 12;
-    auto& wf = g_ctx.wf;
+    auto& wf = ctx().wf;
     if (wf.bytes < need) {
         if (wf.buf) (void)hipFree(wf.buf);
         wf.buf = nullptr;
@@ -1526,7 +1556,7 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
                   hipStream_t s, float4* colours_out = nullptr) {
     int rc = validate(d);
     if (rc) return rc;
-    if (!g_ctx.ready) return fail(LRT_E_STATE, "lrt_initialize() has not been called");
+    if (!ctx().ready) return fail(LRT_E_STATE, "lrt_initialize() has not been called");
     if (!d_buf || !d_rays) return fail(LRT_E_INVALID, "device buffer / ray counter is NULL");
     if (d->x_count == 0 || d->row_count == 0 || d->frames == 0) return LRT_OK;
     KernelArgs a;
@@ -1539,11 +1569,11 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     a.cam.horiz = f3(c.horizontalVec.x, c.horizontalVec.y, c.horizontalVec.z);
     a.cam.vert = f3(c.verticalVec.x, c.verticalVec.y, c.verticalVec.z);
     a.cam.lensRadius = c.lensRadius;
-    a.sph = g_ctx.d_sph;
-    a.mats = g_ctx.d_mats;
-    a.lights = g_ctx.d_lights;
-    a.count = g_ctx.count;
-    a.nlights = g_ctx.nlights;
+    a.sph = ctx().d_sph;
+    a.mats = ctx().d_mats;
+    a.lights = ctx().d_lights;
+    a.count = ctx().count;
+    a.nlights = ctx().nlights;
     a.width = d->width;
     a.height = d->height;
     a.x0 = d->x0;
@@ -1570,23 +1600,23 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
         }
         a.featMax = feat ? feat->max_frame : -1;
     }
-    a.bv.nodes = g_ctx.d_bvh_nodes;
-    a.bv.lsph = g_ctx.d_bvh_lsph;
-    a.bv.lid = g_ctx.d_bvh_lid;
-    a.bv.margin = g_ctx.bvh_margin;
-    a.bv.on = (g_ctx.bvh_on && !(d->flags & LRT_F_NO_BVH)) ? 1 : 0;
-    a.bv.nnodes = g_ctx.bvh_nodes;
-    a.bv.big0 = g_ctx.bvh_big0;
-    a.bv.nbig = g_ctx.bvh_nbig;
+    a.bv.nodes = ctx().d_bvh_nodes;
+    a.bv.lsph = ctx().d_bvh_lsph;
+    a.bv.lid = ctx().d_bvh_lid;
+    a.bv.margin = ctx().bvh_margin;
+    a.bv.on = (ctx().bvh_on && !(d->flags & LRT_F_NO_BVH)) ? 1 : 0;
+    a.bv.nnodes = ctx().bvh_nodes;
+    a.bv.big0 = ctx().bvh_big0;
+    a.bv.nbig = ctx().bvh_nbig;
     a.bvh_stack_offset = 0;
     const bool lds = !(d->flags & LRT_F_SCENE_GLOBAL) &&
                      sizeof(float4) * (kTraceLdsLevels * kBlock + 4 * (size_t)a.count + a.nlights / 4 + 1) <= 64 * 1024;
-    // Kernel policy (measured): v0 -- frames split over lanes, persistent single-wave
-    // blocks on spread tile queues, 4 waves/SIMD -- is fastest on every BASELINE config.
-    // v3 (regeneration) and v4 (wavefront) stay selectable for A/B; the round-1 per-lane
-    // state machines (v1/v2/v2s, always slower) were removed and their flags are rejected.
+    // Kernel policy (auto_kernel, measured): v5 (pool) for calls with >= 4 frames and >= 2
+    // tiles per resident wave, v0 otherwise; v4 (wavefront) stays selectable for A/B. The
+    // round-1 per-lane state machines (v1/v2/v2s) and round-1's v3 regeneration kernel (slower
+    // than v0 or v5 on every config) were removed: their flags are rejected.
     a.regenMin = 0;
-    a.lerp = g_ctx.d_lerp;
+    a.lerp = ctx().d_lerp;
     a.colbuf = nullptr;
     a.poolSlots = 0;
     a.perm = nullptr;
@@ -1598,9 +1628,9 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
         if (d->max_depth <= 8) return launch_depth<8, 1>(a, lds, d->x_count, d->row_count, s);
         return launch_depth<64, 1>(a, lds, d->x_count, d->row_count, s);
     }
-    if (d->flags & (LRT_F_V1 | LRT_F_V2S | LRT_F_V2))
-        return fail(LRT_E_INVALID, "LRT_F_V1/LRT_F_V2S/LRT_F_V2 kernels were removed (use LRT_F_SIMPLE, the default)");
-    int kflags = d->flags & (LRT_F_SIMPLE | LRT_F_V3 | LRT_F_WAVEFRONT | LRT_F_POOL);
+    if (d->flags & (LRT_F_V1 | LRT_F_V2S | LRT_F_V2 | LRT_F_V3))
+        return fail(LRT_E_INVALID, "LRT_F_V1/LRT_F_V2S/LRT_F_V2/LRT_F_V3 kernels were removed (the default picks v0 or v5)");
+    int kflags = d->flags & (LRT_F_SIMPLE | LRT_F_WAVEFRONT | LRT_F_POOL);
     if (kflags == 0) kflags = auto_kernel(a, d, want_feat);
     if (want_feat && !(kflags & LRT_F_SIMPLE))
         return fail(LRT_E_INVALID, "features are implemented by the v0 kernel only");
@@ -1609,10 +1639,6 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
         a.colbuf = nullptr;
         if (d->max_depth <= 8) return launch_pool_split<8>(a, lds, d->x_count, d->row_count, d->frames, s);
         return launch_pool_split<64>(a, lds, d->x_count, d->row_count, d->frames, s);
-    }
-    if (kflags & LRT_F_V3) {
-        if (d->max_depth <= 8) return launch_regen_split<8>(a, lds, d->x_count, d->row_count, d->frames, s);
-        return launch_regen_split<64>(a, lds, d->x_count, d->row_count, d->frames, s);
     }
     if (d->max_depth <= 8) return launch_split<8>(a, lds, d->x_count, d->row_count, d->frames, want_feat, s);
     // depth 9..64: one instance (MAXD only decides whether stack levels beyond the 8 in LDS
@@ -1633,17 +1659,17 @@ int auto_kernel(const KernelArgs& a, const lrt_render_desc* d, bool feat) {
     while (pix > 1 && pix * d->frames > kPoolSamples) pix /= (pix == 64 || pix == 32 ? 2 : 4);
     const int tx = pix >= 32 ? 8 : pix >= 8 ? 4 : pix >= 2 ? 2 : 1, ty = pix / tx;
     const long long tiles = (long long)((d->x_count + tx - 1) / tx) * ((d->row_count + ty - 1) / ty);
-    const long long slots = 16LL * g_ctx.num_cus;   // resident waves (4 per SIMD)
+    const long long slots = 16LL * ctx().num_cus;   // resident waves (4 per SIMD)
     return tiles >= 2 * slots ? LRT_F_POOL : LRT_F_SIMPLE;
 }
 
 int ensure_frame(size_t bytes) {
-    if (g_ctx.frame_bytes >= bytes) return LRT_OK;
-    if (g_ctx.d_frame) (void)hipFree(g_ctx.d_frame);
-    g_ctx.d_frame = nullptr;
-    g_ctx.frame_bytes = 0;
-    if (hipMalloc(&g_ctx.d_frame, bytes) != hipSuccess) return fail(LRT_E_NOMEM, "hipMalloc(frame) failed");
-    g_ctx.frame_bytes = bytes;
+    if (ctx().frame_bytes >= bytes) return LRT_OK;
+    if (ctx().d_frame) (void)hipFree(ctx().d_frame);
+    ctx().d_frame = nullptr;
+    ctx().frame_bytes = 0;
+    if (hipMalloc(&ctx().d_frame, bytes) != hipSuccess) return fail(LRT_E_NOMEM, "hipMalloc(frame) failed");
+    ctx().frame_bytes = bytes;
     return LRT_OK;
 }
 
@@ -1657,6 +1683,67 @@ float* host_pinned(float* buf) {
     }
     if (at.type != hipMemoryTypeHost) return nullptr;
     return at.devicePointer ? (float*)at.devicePointer : buf;
+}
+
+// Registration cache for pageable DrawTest buffers. The reference's caller allocates its
+// backbuffer with `new float[]` once (main.cpp:40) and hands the same pointer to every
+// DrawTest (main.cpp:165); pageable memory can only be staged (H2D + render + D2H: 0.77 ms
+// per 1280x720 frame). A pageable buffer seen by two consecutive lrt_draw_test
+// calls is page-locked in place (hipHostRegister, portable to every device in use) and from
+// then on takes the page-locked paths (pipelined DMA + lerp written over PCIe: 0.52 ms).
+// A registered range must not be freed while registered -- the GPU would later address
+// pages the process no longer maps -- so the contract is DrawTest's own (one buffer for the
+// run): lrt_host_unregister drops one before the caller frees it (the Python binding does it
+// when the array dies), lrt_shutdown drops all, at most kHostRegs stay registered (least
+// recently used dropped first). lrt_render_host never registers. LRT_HOST_REGISTER=0: off.
+struct HostReg {
+    void* p = nullptr;
+    size_t bytes = 0;
+    unsigned long long tick = 0;
+};
+constexpr int kHostRegs = 8;
+HostReg g_host_regs[kHostRegs];
+unsigned long long g_host_reg_tick = 0;
+HostReg g_host_last;   // the last pageable buffer rendered (registered when seen again)
+
+bool host_register_on() {
+    static const bool on = [] {
+        const char* e = getenv("LRT_HOST_REGISTER");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
+int host_unregister(void* p) {
+    for (auto& r : g_host_regs)
+        if (r.p == p) {
+            const hipError_t e = hipHostUnregister(r.p);
+            r = HostReg();
+            if (e != hipSuccess) return hip_fail(e, "hipHostUnregister");
+            return LRT_OK;
+        }
+    return fail(LRT_E_INVALID, "not a buffer the library registered");
+}
+
+// The device address of pageable buf once it is registered (see above), else nullptr.
+float* host_register(float* buf, size_t bytes) {
+    if (!host_register_on()) return nullptr;
+    const bool again = g_host_last.p == buf && g_host_last.bytes == bytes;
+    g_host_last.p = buf;
+    g_host_last.bytes = bytes;
+    if (!again) return nullptr;
+    HostReg* slot = &g_host_regs[0];
+    for (auto& r : g_host_regs)
+        if (r.tick < slot->tick) slot = &r;
+    if (slot->p) (void)host_unregister(slot->p);
+    if (hipHostRegister(buf, bytes, hipHostRegisterPortable | hipHostRegisterMapped) != hipSuccess) {
+        (void)hipGetLastError();   // e.g. overlaps a registered range: stay on the staged path
+        return nullptr;
+    }
+    slot->p = buf;
+    slot->bytes = bytes;
+    slot->tick = ++g_host_reg_tick;
+    return host_pinned(buf);
 }
 
 // Page-locked host backbuffers are rendered in place (zero copy): the kernel's 16 B read
@@ -1689,11 +1776,11 @@ bool host_pipeline(const lrt_render_desc* d, size_t bytes) {
         const char* e = getenv("LRT_HOST_PIPELINE");
         return e ? atoi(e) : 1;
     }();
-    const bool bvh = g_ctx.bvh_on && !(d->flags & LRT_F_NO_BVH);
+    const bool bvh = ctx().bvh_on && !(d->flags & LRT_F_NO_BVH);
     const bool lds = !(d->flags & LRT_F_SCENE_GLOBAL) &&
-                     sizeof(float4) * (kTraceLdsLevels * kBlock + 4 * (size_t)g_ctx.count + g_ctx.nlights / 4 + 1) <=
+                     sizeof(float4) * (kTraceLdsLevels * kBlock + 4 * (size_t)ctx().count + ctx().nlights / 4 + 1) <=
                          64 * 1024;
-    const int kflags = d->flags & (LRT_F_SIMPLE | LRT_F_V3 | LRT_F_WAVEFRONT | LRT_F_POOL);
+    const int kflags = d->flags & (LRT_F_SIMPLE | LRT_F_WAVEFRONT | LRT_F_POOL);
     return mode != 0 && d->frames <= 4 && bytes * (size_t)d->frames <= (256u << 20) && !bvh && lds &&
            (kflags == 0 || kflags == LRT_F_SIMPLE) && !(d->flags & LRT_F_NO_DOUBLE_LIGHT) &&
            d->row_count >= Context::kHostChunks;
@@ -1709,19 +1796,19 @@ int host_chunks() {   // row chunks of the DMA copy (LRT_HOST_CHUNKS, 1..8)
 }
 
 int render_host_pipelined(const lrt_render_desc* d, float* buf, float* hdev, size_t bytes, long long* out_rays) {
-    hipStream_t s = g_ctx.stream;
-    if (!g_ctx.s_in) {
-        LRT_HIP(hipStreamCreateWithFlags(&g_ctx.s_in, hipStreamNonBlocking));
+    hipStream_t s = ctx().stream;
+    if (!ctx().s_in) {
+        LRT_HIP(hipStreamCreateWithFlags(&ctx().s_in, hipStreamNonBlocking));
         for (int c = 0; c < Context::kHostChunks; ++c)
-            LRT_HIP(hipEventCreateWithFlags(&g_ctx.ev_in[c], hipEventDisableTiming));
+            LRT_HIP(hipEventCreateWithFlags(&ctx().ev_in[c], hipEventDisableTiming));
     }
     const size_t cbytes = bytes * (size_t)d->frames;
-    if (g_ctx.col_bytes < cbytes) {
-        if (g_ctx.d_col) (void)hipFree(g_ctx.d_col);
-        g_ctx.d_col = nullptr;
-        g_ctx.col_bytes = 0;
-        if (hipMalloc(&g_ctx.d_col, cbytes) != hipSuccess) return fail(LRT_E_NOMEM, "hipMalloc(sample colours)");
-        g_ctx.col_bytes = cbytes;
+    if (ctx().col_bytes < cbytes) {
+        if (ctx().d_col) (void)hipFree(ctx().d_col);
+        ctx().d_col = nullptr;
+        ctx().col_bytes = 0;
+        if (hipMalloc(&ctx().d_col, cbytes) != hipSuccess) return fail(LRT_E_NOMEM, "hipMalloc(sample colours)");
+        ctx().col_bytes = cbytes;
     }
     const int K = host_chunks(), rows = d->row_count, xc = d->x_count;
     const size_t npix = (size_t)xc * rows;
@@ -1733,59 +1820,205 @@ int render_host_pipelined(const lrt_render_desc* d, float* buf, float* hdev, siz
     for (int c = 0; c < K; ++c) {   // previous values, host -> device (DMA), beside the render
         size_t p0, n;
         chunk(c, p0, n);
-        LRT_HIP(hipMemcpyAsync(g_ctx.d_frame + 4 * p0, buf + 4 * p0, n * 16, hipMemcpyHostToDevice, g_ctx.s_in));
-        LRT_HIP(hipEventRecord(g_ctx.ev_in[c], g_ctx.s_in));
+        LRT_HIP(hipMemcpyAsync(ctx().d_frame + 4 * p0, buf + 4 * p0, n * 16, hipMemcpyHostToDevice, ctx().s_in));
+        LRT_HIP(hipEventRecord(ctx().ev_in[c], ctx().s_in));
     }
-    LRT_HIP(hipMemsetAsync(g_ctx.d_rays, 0, sizeof(unsigned long long), s));
-    int rc = render_device(d, g_ctx.d_frame, g_ctx.d_rays, nullptr, s, g_ctx.d_col);
+    LRT_HIP(hipMemsetAsync(ctx().d_rays, 0, sizeof(unsigned long long), s));
+    int rc = render_device(d, ctx().d_frame, ctx().d_rays, nullptr, s, ctx().d_col);
     if (rc) {
-        (void)hipStreamSynchronize(g_ctx.s_in);
+        (void)hipStreamSynchronize(ctx().s_in);
         return rc;
     }
     for (int c = 0; c < K; ++c) {   // each chunk's lerp once its values are in, written to the host pixels
         size_t p0, n;
         chunk(c, p0, n);
-        LRT_HIP(hipStreamWaitEvent(s, g_ctx.ev_in[c], 0));
+        LRT_HIP(hipStreamWaitEvent(s, ctx().ev_in[c], 0));
         merge_to_host_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(
-            g_ctx.d_col + p0, reinterpret_cast<const float4*>(g_ctx.d_frame) + p0, reinterpret_cast<float4*>(hdev) + p0,
-            g_ctx.d_lerp, (int)n, d->frame0, d->frames, npix);
+            ctx().d_col + p0, reinterpret_cast<const float4*>(ctx().d_frame) + p0, reinterpret_cast<float4*>(hdev) + p0,
+            ctx().d_lerp, (int)n, d->frame0, d->frames, npix);
         LRT_HIP(hipGetLastError());
     }
     unsigned long long rays = 0;
-    LRT_HIP(hipMemcpyAsync(&rays, g_ctx.d_rays, sizeof(rays), hipMemcpyDeviceToHost, s));
+    LRT_HIP(hipMemcpyAsync(&rays, ctx().d_rays, sizeof(rays), hipMemcpyDeviceToHost, s));
     LRT_HIP(hipStreamSynchronize(s));
     if (out_rays) *out_rays = (long long)rays;
     return LRT_OK;
 }
 
-int render_host(const lrt_render_desc* d, float* buf, long long* out_rays, const lrt_features* feat = nullptr) {
+// Makes context k the one ctx() returns and its device the calling thread's current one, for
+// the scope's lifetime (both restored after).
+struct DeviceScope {
+    int prev_cur, prev_dev = -1;
+    explicit DeviceScope(int k) : prev_cur(g_cur) {
+        g_cur = k;
+        int dev = 0;
+        if (hipGetDevice(&dev) == hipSuccess && dev != g_devs[k].device) {
+            prev_dev = dev;
+            (void)hipSetDevice(g_devs[k].device);
+        }
+    }
+    ~DeviceScope() {
+        if (prev_dev >= 0) (void)hipSetDevice(prev_dev);
+        g_cur = prev_cur;
+    }
+};
+
+int ensure_buffer(float*& p, size_t& have, size_t bytes, const char* what) {
+    if (have >= bytes) return LRT_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    have = 0;
+    if (hipMalloc(&p, bytes) != hipSuccess) return fail(LRT_E_NOMEM, std::string("hipMalloc(") + what + ")");
+    have = bytes;
+    return LRT_OK;
+}
+
+// One host render split over the g_ndev devices of lrt_initialize_devices (BASELINE config 5:
+// "row-tiled across 8xMI355X with RCCL gather over xGMI"). The caller's rows are dealt in
+// blocks of g_multi.row_block rows round-robin (row-block-cyclic: contiguous bands are
+// imbalanced); device k
+//   1. receives the previous values of its rows from the caller's buffer (one strided DMA),
+//   2. renders them densely into its shard buffer (lrt_render_desc's row map: row_period =
+//      N, row_phase = k; any kernel the policy picks),
+// then ONE collective brings the shards to device 0: a grouped ncclGather over RCCL
+// (rccl.h:745) when the devices are distinct, device-to-device copies when a device is
+// listed twice (RCCL refuses two ranks on one GPU: the 1-GPU rehearsal); device 0 assembles
+// the frame (unshard_kernel) and copies it to the caller. Per-pixel seeds make the frame
+// bit-identical to a 1-device render for any N and block size.
+int render_host_multi_enqueue(const lrt_render_desc* d, float* buf, size_t bytes, unsigned long long* rays);
+int render_host_multi(const lrt_render_desc* d, float* buf, size_t bytes, long long* out_rays) {
+    std::vector<unsigned long long> rays(g_ndev, 0ull);
+    const int rc = render_host_multi_enqueue(d, buf, bytes, rays.data());
+    long long total = 0;
+    for (int k = 0; k < g_ndev; ++k) {   // also after a failure: nothing may still write `rays`
+        DeviceScope ds(k);
+        const hipError_t e = hipStreamSynchronize(ctx().stream);
+        if (e != hipSuccess && rc == LRT_OK) return hip_fail(e, "hipStreamSynchronize(multi-device render)");
+        total += (long long)rays[k];
+    }
+    if (rc) return rc;
+    snprintf(g_last_launch + strlen(g_last_launch), sizeof(g_last_launch) - strlen(g_last_launch),
+             " devices=%d exchange=%s row_block=%d", g_ndev, g_multi.rccl ? "rccl" : "copy", g_multi.row_block);
+    if (out_rays) *out_rays = total;
+    return LRT_OK;
+}
+int render_host_multi_enqueue(const lrt_render_desc* d, float* buf, size_t bytes, unsigned long long* rays) {
+    const int N = g_ndev, b = g_multi.row_block, xc = d->x_count, rows = d->row_count;
+    const size_t rowBytes = (size_t)xc * 16;
+    const int maxRows = lrt_shard_rows(rows, b, N, 0);
+    const size_t shardBytes = (size_t)maxRows * rowBytes;
+    for (int k = 0; k < N; ++k) {
+        DeviceScope ds(k);
+        Context& c = ctx();
+        if (int rc = ensure_buffer(c.d_shard, c.shard_bytes, shardBytes, "shard")) return rc;
+        if (!c.ev_done) LRT_HIP(hipEventCreateWithFlags(&c.ev_done, hipEventDisableTiming));
+        const int rk = lrt_shard_rows(rows, b, N, k);
+        if (rk > 0) {
+            // shard row j is the caller's row (j / b) * b * N + k * b + j % b: whole blocks
+            // are one 2D copy (pitch N blocks), a last partial block one more
+            const int full = rk / b, tail = rk % b;
+            const size_t blk = (size_t)b * rowBytes;
+            const char* src = reinterpret_cast<const char*>(buf) + (size_t)k * blk;
+            if (full > 0)
+                LRT_HIP(hipMemcpy2DAsync(c.d_shard, blk, src, blk * N, blk, (size_t)full, hipMemcpyHostToDevice,
+                                         c.stream));
+            if (tail > 0)
+                LRT_HIP(hipMemcpyAsync(reinterpret_cast<char*>(c.d_shard) + (size_t)full * blk,
+                                       src + (size_t)full * blk * N, (size_t)tail * rowBytes, hipMemcpyHostToDevice,
+                                       c.stream));
+        }
+        LRT_HIP(hipMemsetAsync(c.d_rays, 0, sizeof(unsigned long long), c.stream));
+        lrt_render_desc sd = *d;
+        sd.row_count = rk;
+        sd.row_block = b;
+        sd.row_period = N;
+        sd.row_phase = k;
+        if (int rc = render_device(&sd, c.d_shard, c.d_rays, nullptr, c.stream)) return rc;
+        LRT_HIP(hipMemcpyAsync(&rays[k], c.d_rays, sizeof(unsigned long long), hipMemcpyDeviceToHost, c.stream));
+        LRT_HIP(hipEventRecord(c.ev_done, c.stream));
+    }
+    {   // the exchange: every shard into device 0's gather buffer
+        DeviceScope ds0(0);
+        Context& c0 = ctx();
+        if (int rc = ensure_buffer(c0.d_gath, c0.gath_bytes, shardBytes * N, "gather")) return rc;
+        if (int rc = ensure_frame(bytes)) return rc;
+        if (g_multi.rccl) {
+            const size_t count = shardBytes / sizeof(float);
+            if (ncclGroupStart() != ncclSuccess) return fail(LRT_E_HIP, "ncclGroupStart");
+            ncclResult_t r = ncclSuccess;
+            for (int k = 0; k < N && r == ncclSuccess; ++k) {
+                DeviceScope ds(k);
+                r = ncclGather(g_devs[k].d_shard, k == 0 ? c0.d_gath : nullptr, count, ncclFloat, 0, g_multi.comms[k],
+                               g_devs[k].stream);
+            }
+            const ncclResult_t r2 = ncclGroupEnd();
+            if (r != ncclSuccess || r2 != ncclSuccess)
+                return fail(LRT_E_HIP, std::string("ncclGather: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+        } else {
+            for (int k = 0; k < N; ++k) {
+                LRT_HIP(hipStreamWaitEvent(c0.stream, g_devs[k].ev_done, 0));
+                char* dst = reinterpret_cast<char*>(c0.d_gath) + (size_t)k * shardBytes;
+                if (g_devs[k].device == c0.device)
+                    LRT_HIP(hipMemcpyAsync(dst, g_devs[k].d_shard, shardBytes, hipMemcpyDeviceToDevice, c0.stream));
+                else
+                    LRT_HIP(hipMemcpyPeerAsync(dst, c0.device, g_devs[k].d_shard, g_devs[k].device, shardBytes,
+                                               c0.stream));
+            }
+        }
+        dim3 grid((unsigned)((xc + 255) / 256), (unsigned)rows);
+        unshard_kernel<<<grid, 256, 0, c0.stream>>>(reinterpret_cast<const float4*>(c0.d_gath),
+                                                   reinterpret_cast<float4*>(c0.d_frame), xc, rows, b, N, maxRows);
+        LRT_HIP(hipGetLastError());
+        LRT_HIP(hipMemcpyAsync(buf, c0.d_frame, bytes, hipMemcpyDeviceToHost, c0.stream));
+    }
+    return LRT_OK;
+}
+
+// allow_register: the reference API's call (lrt_draw_test), whose caller keeps one buffer for
+// the whole run (main.cpp:40,165): a pageable buffer may be page-locked (host_register).
+int render_host(const lrt_render_desc* d, float* buf, long long* out_rays, const lrt_features* feat = nullptr,
+                bool allow_register = false) {
     int rc = validate(d);
     if (rc) return rc;
-    if (!g_ctx.ready) return fail(LRT_E_STATE, "lrt_initialize() has not been called");
+    if (!ctx().ready) return fail(LRT_E_STATE, "lrt_initialize() has not been called");
     if (!buf) return fail(LRT_E_INVALID, "backbuffer is NULL");
     const size_t bytes = (size_t)d->x_count * d->row_count * 4 * sizeof(float);
     if (bytes == 0 || d->frames == 0) {
         if (out_rays) *out_rays = 0;
         return LRT_OK;
     }
+    // lrt_initialize_devices: the caller's rows are split over every device (a window of
+    // contiguous rows; a caller's own row-block-cyclic shard, or features, stay on device 0)
+    if (g_multi.on && d->row_period == 1 && !feat) return render_host_multi(d, buf, bytes, out_rays);
+    // lrt_last_launch() names the host path too: host=pipelined | zerocopy | staged, with
+    // "registered-" when the registration cache page-locked a pageable buffer
+    auto note = [](const char* path, bool registered) {
+        const size_t n = strlen(g_last_launch);
+        snprintf(g_last_launch + n, sizeof(g_last_launch) - n, " host=%s%s", registered ? "registered-" : "", path);
+    };
     float* hdev = (!feat && host_zero_copy()) ? host_pinned(buf) : nullptr;
+    const bool registered =
+        allow_register && !hdev && !feat && host_zero_copy() && (hdev = host_register(buf, bytes)) != nullptr;
     if (hdev && host_pipeline(d, bytes)) {
         if ((rc = ensure_frame(bytes))) return rc;
-        return render_host_pipelined(d, buf, hdev, bytes, out_rays);
+        if ((rc = render_host_pipelined(d, buf, hdev, bytes, out_rays))) return rc;
+        note("pipelined", registered);
+        return LRT_OK;
     }
     if (hdev) {   // zero copy: the kernel reads and writes the caller's pixels over PCIe
-        LRT_HIP(hipMemsetAsync(g_ctx.d_rays, 0, sizeof(unsigned long long), g_ctx.stream));
-        if ((rc = render_device(d, hdev, g_ctx.d_rays, nullptr, g_ctx.stream))) return rc;
+        LRT_HIP(hipMemsetAsync(ctx().d_rays, 0, sizeof(unsigned long long), ctx().stream));
+        if ((rc = render_device(d, hdev, ctx().d_rays, nullptr, ctx().stream))) return rc;
         unsigned long long rays = 0;
-        LRT_HIP(hipMemcpyAsync(&rays, g_ctx.d_rays, sizeof(rays), hipMemcpyDeviceToHost, g_ctx.stream));
-        LRT_HIP(hipStreamSynchronize(g_ctx.stream));
+        LRT_HIP(hipMemcpyAsync(&rays, ctx().d_rays, sizeof(rays), hipMemcpyDeviceToHost, ctx().stream));
+        LRT_HIP(hipStreamSynchronize(ctx().stream));
         if (out_rays) *out_rays = (long long)rays;
+        note("zerocopy", registered);
         return LRT_OK;
     }
     if ((rc = ensure_frame(bytes))) return rc;
-    hipStream_t s = g_ctx.stream;
-    LRT_HIP(hipMemcpyAsync(g_ctx.d_frame, buf, bytes, hipMemcpyHostToDevice, s));
-    LRT_HIP(hipMemsetAsync(g_ctx.d_rays, 0, sizeof(unsigned long long), s));
+    hipStream_t s = ctx().stream;
+    LRT_HIP(hipMemcpyAsync(ctx().d_frame, buf, bytes, hipMemcpyHostToDevice, s));
+    LRT_HIP(hipMemsetAsync(ctx().d_rays, 0, sizeof(unsigned long long), s));
     // host feature buffers go through device mirrors like the backbuffer
     lrt_features dfeat;
     memset(&dfeat, 0, sizeof(dfeat));
@@ -1798,25 +2031,26 @@ int render_host(const lrt_render_desc* d, float* buf, long long* out_rays, const
         dfeat.max_frame = feat->max_frame;
         for (int k = 0; k < 6; ++k) {
             if (!hp[k]) continue;
-            if (g_ctx.feat_bytes[k] < bytes) {
-                if (g_ctx.d_feat[k]) (void)hipFree(g_ctx.d_feat[k]);
-                g_ctx.d_feat[k] = nullptr;
-                g_ctx.feat_bytes[k] = 0;
-                if (hipMalloc(&g_ctx.d_feat[k], bytes) != hipSuccess) return fail(LRT_E_NOMEM, "hipMalloc(features)");
-                g_ctx.feat_bytes[k] = bytes;
+            if (ctx().feat_bytes[k] < bytes) {
+                if (ctx().d_feat[k]) (void)hipFree(ctx().d_feat[k]);
+                ctx().d_feat[k] = nullptr;
+                ctx().feat_bytes[k] = 0;
+                if (hipMalloc(&ctx().d_feat[k], bytes) != hipSuccess) return fail(LRT_E_NOMEM, "hipMalloc(features)");
+                ctx().feat_bytes[k] = bytes;
             }
-            *dp[k] = g_ctx.d_feat[k];
-            LRT_HIP(hipMemcpyAsync(g_ctx.d_feat[k], hp[k], bytes, hipMemcpyHostToDevice, s));
+            *dp[k] = ctx().d_feat[k];
+            LRT_HIP(hipMemcpyAsync(ctx().d_feat[k], hp[k], bytes, hipMemcpyHostToDevice, s));
         }
     }
-    if ((rc = render_device(d, g_ctx.d_frame, g_ctx.d_rays, feat ? &dfeat : nullptr, s))) return rc;
+    if ((rc = render_device(d, ctx().d_frame, ctx().d_rays, feat ? &dfeat : nullptr, s))) return rc;
     unsigned long long rays = 0;
-    LRT_HIP(hipMemcpyAsync(buf, g_ctx.d_frame, bytes, hipMemcpyDeviceToHost, s));
+    LRT_HIP(hipMemcpyAsync(buf, ctx().d_frame, bytes, hipMemcpyDeviceToHost, s));
     for (int k = 0; k < 6; ++k)
-        if (hp[k]) LRT_HIP(hipMemcpyAsync(hp[k], g_ctx.d_feat[k], bytes, hipMemcpyDeviceToHost, s));
-    LRT_HIP(hipMemcpyAsync(&rays, g_ctx.d_rays, sizeof(rays), hipMemcpyDeviceToHost, s));
+        if (hp[k]) LRT_HIP(hipMemcpyAsync(hp[k], ctx().d_feat[k], bytes, hipMemcpyDeviceToHost, s));
+    LRT_HIP(hipMemcpyAsync(&rays, ctx().d_rays, sizeof(rays), hipMemcpyDeviceToHost, s));
     LRT_HIP(hipStreamSynchronize(s));
     if (out_rays) *out_rays = (long long)rays;
+    note("staged", false);
     return LRT_OK;
 }
 
@@ -1902,40 +2136,23 @@ __global__ __launch_bounds__(64) void bvh_probe_kernel(BvhView bv, const float* 
     ts[i] = t;
 }
 
-}  // namespace lrt
 
-using namespace lrt;
-
-// roctx ranges around the C-ABI's work entry points (SURVEY §5 tracing): rocprofv3
-// --marker-trace shows each lrt_* call on the host timeline above the kernels it launched.
-struct RoctxRange {
-    explicit RoctxRange(const char* name) { roctxRangePushA(name); }
-    ~RoctxRange() { roctxRangePop(); }
-};
-
-extern "C" {
-
-const char* lrt_last_error(void) { return t_err.c_str(); }
-const char* lrt_version(void) { return LRT_VERSION_STRING; }
-const char* lrt_last_launch(void) { return g_last_launch; }
-
-int lrt_initialize(void) {
-    std::lock_guard<std::mutex> lk(g_mu);
-    if (g_ctx.ready) return LRT_OK;
-    int dev = 0;
-    LRT_HIP(hipGetDevice(&dev));
-    g_ctx.device = dev;
-    LRT_HIP(hipStreamCreateWithFlags(&g_ctx.stream, hipStreamNonBlocking));
-    LRT_HIP(hipMalloc(&g_ctx.d_rays, sizeof(unsigned long long)));
-    LRT_HIP(hipMalloc(&g_ctx.d_tiles, sizeof(unsigned long long) * kQueueSlots * kTileSetU64));
-    LRT_HIP(hipMemset(g_ctx.d_tiles, 0, sizeof(unsigned long long) * kQueueSlots * kTileSetU64));
+// A device's context: its stream, counters, lerp table and the default scene (lrt_initialize,
+// and each device of lrt_initialize_devices; the device is current).
+int init_context(Context& c, int dev) {
+    c = Context();
+    c.device = dev;
+    LRT_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    LRT_HIP(hipMalloc(&c.d_rays, sizeof(unsigned long long)));
+    LRT_HIP(hipMalloc(&c.d_tiles, sizeof(unsigned long long) * kQueueSlots * kTileSetU64));
+    LRT_HIP(hipMemset(c.d_tiles, 0, sizeof(unsigned long long) * kQueueSlots * kTileSetU64));
     {   // parallel.cpp:262's lerpFac per frame number, divided once here instead of per wave
         std::vector<float> t(kLerpTable);
         for (int f = 0; f < kLerpTable; ++f) t[f] = (float)f / (float)(f + 1);
-        LRT_HIP(hipMalloc(&g_ctx.d_lerp, sizeof(float) * kLerpTable));
-        LRT_HIP(hipMemcpy(g_ctx.d_lerp, t.data(), sizeof(float) * kLerpTable, hipMemcpyHostToDevice));
+        LRT_HIP(hipMalloc(&c.d_lerp, sizeof(float) * kLerpTable));
+        LRT_HIP(hipMemcpy(c.d_lerp, t.data(), sizeof(float) * kLerpTable, hipMemcpyHostToDevice));
     }
-    LRT_HIP(hipDeviceGetAttribute(&g_ctx.num_cus, hipDeviceAttributeMultiprocessorCount, dev));
+    LRT_HIP(hipDeviceGetAttribute(&c.num_cus, hipDeviceAttributeMultiprocessorCount, dev));
     {   // keep freed stream-ordered blocks (the per-launch path-stack overflow) in the
         // pool instead of returning them to the driver at every synchronisation
         hipMemPool_t pool;
@@ -1944,39 +2161,175 @@ int lrt_initialize(void) {
             (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
         }
     }
-    int rc = upload_scene(g_ctx, kDefaultSpheres, kDefaultMats, 9);
-    if (rc) return rc;
-    g_ctx.ready = true;
+    if (int rc = upload_scene(c, kDefaultSpheres, kDefaultMats, 9)) return rc;
+    c.ready = true;
     return LRT_OK;
+}
+
+// Frees everything init_context and the render paths allocated (the device is current).
+void free_context(Context& c) {
+    if (c.stream) (void)hipStreamSynchronize(c.stream);
+    (void)hipDeviceSynchronize();
+    free_scene(c);
+    for (float* p : {c.d_frame, c.d_shard, c.d_gath})
+        if (p) (void)hipFree(p);
+    if (c.d_rays) (void)hipFree(c.d_rays);
+    if (c.d_tiles) (void)hipFree(c.d_tiles);
+    if (c.d_lerp) (void)hipFree(c.d_lerp);
+    if (c.wf.buf) (void)hipFree(c.wf.buf);
+    if (c.wf.rayp) (void)hipFree(c.wf.rayp);
+    for (auto* f : c.d_feat)
+        if (f) (void)hipFree(f);
+    for (auto& m : c.masked_streams) (void)hipStreamDestroy(m.first);
+    if (c.d_col) (void)hipFree(c.d_col);
+    for (auto& o : c.order) {
+        if (o.d_cost) (void)hipFree(o.d_cost);
+        if (o.d_perm) (void)hipFree(o.d_perm);
+        if (o.ev_rec) (void)hipEventDestroy(o.ev_rec);
+        for (auto& u : o.uses) (void)hipEventDestroy(u.second);
+    }
+    for (int k = 0; k < Context::kHostChunks; ++k)
+        if (c.ev_in[k]) (void)hipEventDestroy(c.ev_in[k]);
+    if (c.ev_done) (void)hipEventDestroy(c.ev_done);
+    if (c.s_in) (void)hipStreamDestroy(c.s_in);
+    if (c.stream) (void)hipStreamDestroy(c.stream);
+    c = Context();
+}
+}  // namespace lrt
+
+using namespace lrt;
+
+// roctx ranges around the C-ABI's work entry points (SURVEY §5 tracing): rocprofv3
+// --marker-trace shows each lrt_* call on the host timeline above the kernels it launched.
+struct RoctxRange {
+#if LRT_ROCTX
+    explicit RoctxRange(const char* name) { roctxRangePushA(name); }
+    ~RoctxRange() { roctxRangePop(); }
+#else
+    explicit RoctxRange(const char*) {}
+#endif
+};
+
+extern "C" {
+
+const char* lrt_last_error(void) { return t_err.c_str(); }
+const char* lrt_version(void) { return LRT_VERSION_STRING; }
+const char* lrt_last_launch(void) {
+    // a copy taken under the lock: render calls on other threads rewrite g_last_launch
+    std::lock_guard<std::mutex> lk(g_mu);
+    t_launch = g_last_launch;
+    return t_launch.c_str();
+}
+
+int lrt_initialize(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_ndev > 0) return LRT_OK;
+    int dev = 0;
+    LRT_HIP(hipGetDevice(&dev));
+    g_cur = 0;
+    const int rc = init_context(g_devs[0], dev);
+    if (rc) {
+        free_context(g_devs[0]);
+        return rc;
+    }
+    g_ndev = 1;
+    g_multi = Multi();
+    return LRT_OK;
+}
+
+int lrt_initialize_devices(int n, const int* device_ids, int flags) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_ndev > 0) return fail(LRT_E_STATE, "already initialised: call lrt_shutdown() first");
+    if ((flags & ~LRT_DEV_PEER_COPY) != 0) return fail(LRT_E_INVALID, "unknown lrt_initialize_devices flags");
+    int visible = 0;
+    LRT_HIP(hipGetDeviceCount(&visible));
+    std::vector<int> ids;
+    if (n == 0 && !device_ids) {   // every visible device
+        for (int i = 0; i < visible && i < kMaxDevices; ++i) ids.push_back(i);
+    } else {
+        if (n < 1 || n > kMaxDevices || !device_ids) return fail(LRT_E_INVALID, "need 1..16 device ids");
+        ids.assign(device_ids, device_ids + n);
+    }
+    if (ids.empty()) return fail(LRT_E_INVALID, "no device");
+    for (int id : ids)
+        if (id < 0 || id >= visible) return fail(LRT_E_INVALID, "device id out of range");
+    int prev = 0;
+    LRT_HIP(hipGetDevice(&prev));
+    int rc = LRT_OK;
+    int k = 0;
+    for (; k < (int)ids.size() && rc == LRT_OK; ++k) {
+        g_cur = k;
+        if (hipSetDevice(ids[k]) != hipSuccess) {
+            rc = fail(LRT_E_HIP, "hipSetDevice");
+            break;
+        }
+        rc = init_context(g_devs[k], ids[k]);
+    }
+    g_cur = 0;
+    const int N = (int)ids.size();
+    bool distinct = true;
+    for (int i = 0; i < N; ++i)
+        for (int j = 0; j < i; ++j) distinct = distinct && ids[i] != ids[j];
+    g_multi = Multi();
+    if (const char* e = getenv("LRT_ROW_BLOCK")) g_multi.row_block = std::max(1, atoi(e));
+    if (rc == LRT_OK && distinct && !(flags & LRT_DEV_PEER_COPY)) {
+        // one communicator per device, all in this process (the single-thread multi-device
+        // form of RCCL); the gather is issued as a group (render_host_multi)
+        const ncclResult_t r = ncclCommInitAll(g_multi.comms, N, ids.data());
+        if (r != ncclSuccess) rc = fail(LRT_E_HIP, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
+        g_multi.rccl = r == ncclSuccess;
+    } else if (rc == LRT_OK) {
+        for (int i = 1; i < N; ++i)   // peer copies into device 0 (ignore "already enabled")
+            if (ids[i] != ids[0]) {
+                (void)hipSetDevice(ids[0]);
+                (void)hipDeviceEnablePeerAccess(ids[i], 0);
+                (void)hipGetLastError();
+            }
+    }
+    (void)hipSetDevice(prev);
+    if (rc) {
+        for (int i = 0; i < k; ++i) {
+            DeviceScope ds(i);
+            free_context(g_devs[i]);
+        }
+        if (g_multi.rccl)
+            for (int i = 0; i < N; ++i) (void)ncclCommDestroy(g_multi.comms[i]);
+        g_multi = Multi();
+        return rc;
+    }
+    g_ndev = N;
+    g_multi.on = true;
+    return LRT_OK;
+}
+
+int lrt_device_count(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    return g_ndev;
 }
 
 int lrt_shutdown(void) {
     std::lock_guard<std::mutex> lk(g_mu);
-    if (!g_ctx.ready) return LRT_OK;
-    (void)hipDeviceSynchronize();
-    free_scene(g_ctx);
-    if (g_ctx.d_frame) (void)hipFree(g_ctx.d_frame);
-    if (g_ctx.d_rays) (void)hipFree(g_ctx.d_rays);
-    if (g_ctx.d_tiles) (void)hipFree(g_ctx.d_tiles);
-    g_ctx.d_tiles = nullptr;
-    if (g_ctx.d_lerp) (void)hipFree(g_ctx.d_lerp);
-    g_ctx.d_lerp = nullptr;
-    if (g_ctx.wf.buf) (void)hipFree(g_ctx.wf.buf);
-    if (g_ctx.wf.rayp) (void)hipFree(g_ctx.wf.rayp);
-    g_ctx.wf = Context::Wavefront();
-    for (auto* f : g_ctx.d_feat)
-        if (f) (void)hipFree(f);
-    for (auto& m : g_ctx.masked_streams) (void)hipStreamDestroy(m.first);
-    if (g_ctx.d_col) (void)hipFree(g_ctx.d_col);
-    if (g_ctx.order.d_cost) (void)hipFree(g_ctx.order.d_cost);
-    if (g_ctx.order.d_perm) (void)hipFree(g_ctx.order.d_perm);
-    if (g_ctx.order.ev) (void)hipEventDestroy(g_ctx.order.ev);
-    for (int c = 0; c < Context::kHostChunks; ++c)
-        if (g_ctx.ev_in[c]) (void)hipEventDestroy(g_ctx.ev_in[c]);
-    if (g_ctx.s_in) (void)hipStreamDestroy(g_ctx.s_in);
-    if (g_ctx.stream) (void)hipStreamDestroy(g_ctx.stream);
-    g_ctx = Context();
+    if (g_ndev == 0) return LRT_OK;
+    for (auto& r : g_host_regs)
+        if (r.p) (void)host_unregister(r.p);
+    g_host_last = HostReg();
+    if (g_multi.rccl)
+        for (int k = 0; k < g_ndev; ++k) (void)ncclCommDestroy(g_multi.comms[k]);
+    for (int k = 0; k < g_ndev; ++k) {
+        DeviceScope ds(k);
+        free_context(g_devs[k]);
+    }
+    g_ndev = 0;
+    g_cur = 0;
+    g_multi = Multi();
     return LRT_OK;
+}
+
+int lrt_host_unregister(void* p) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!p) return LRT_OK;
+    if (g_host_last.p == p) g_host_last = HostReg();
+    return host_unregister(p);
 }
 
 int lrt_draw_test(float time, int frameCount, int screenWidth, int screenHeight, float* backbuffer,
@@ -1984,6 +2337,7 @@ int lrt_draw_test(float time, int frameCount, int screenWidth, int screenHeight,
     RoctxRange rr_("lrt_draw_test");
     (void)time;   // unused by the reference too (JobData::time, parallel.cpp:244)
     std::lock_guard<std::mutex> lk(g_mu);
+    DeviceScope ds_(0);   // context 0's device (device 0 of lrt_initialize_devices)
     lrt_render_desc d;
     memset(&d, 0, sizeof(d));
     int rc = camera_default(screenWidth, screenHeight, &d.camera);
@@ -2001,7 +2355,7 @@ int lrt_draw_test(float time, int frameCount, int screenWidth, int screenHeight,
     d.frames = 1;
     d.max_depth = LRT_REFERENCE_MAX_DEPTH;
     long long rays = 0;
-    rc = render_host(&d, backbuffer, &rays);
+    rc = render_host(&d, backbuffer, &rays, nullptr, true);
     if (rc) return rc;
     if (outRayCount) *outRayCount = (int)rays;
     return LRT_OK;
@@ -2017,10 +2371,14 @@ int lrt_camera_default(int width, int height, lrt_camera* out) { return camera_d
 int lrt_set_scene(const lrt_sphere* spheres, const lrt_material* materials, int count) {
     RoctxRange rr_("lrt_set_scene");
     std::lock_guard<std::mutex> lk(g_mu);
-    if (!g_ctx.ready) return fail(LRT_E_STATE, "lrt_initialize() has not been called");
-    LRT_HIP(hipStreamSynchronize(g_ctx.stream));
-    LRT_HIP(hipDeviceSynchronize());
-    return upload_scene(g_ctx, spheres, materials, count);
+    if (!ctx().ready) return fail(LRT_E_STATE, "lrt_initialize() has not been called");
+    for (int k = 0; k < g_ndev; ++k) {   // every device in use holds the scene
+        DeviceScope ds(k);
+        LRT_HIP(hipStreamSynchronize(ctx().stream));
+        LRT_HIP(hipDeviceSynchronize());
+        if (int rc = upload_scene(ctx(), spheres, materials, count)) return rc;
+    }
+    return LRT_OK;
 }
 
 int lrt_default_scene(lrt_sphere* spheres, lrt_material* materials, int capacity, int* count) {
@@ -2034,6 +2392,7 @@ int lrt_default_scene(lrt_sphere* spheres, lrt_material* materials, int capacity
 int lrt_render_device(const lrt_render_desc* desc, float* d_backbuffer, unsigned long long* d_rays, void* stream) {
     RoctxRange rr_("lrt_render_device");
     std::lock_guard<std::mutex> lk(g_mu);
+    DeviceScope ds_(0);   // context 0's device (device 0 of lrt_initialize_devices)
     return render_device(desc, d_backbuffer, d_rays, nullptr, (hipStream_t)stream);
 }
 
@@ -2041,6 +2400,7 @@ int lrt_render_device_ex(const lrt_render_desc* desc, float* d_backbuffer, unsig
                          const lrt_features* d_features, void* stream) {
     RoctxRange rr_("lrt_render_device_ex");
     std::lock_guard<std::mutex> lk(g_mu);
+    DeviceScope ds_(0);   // context 0's device (device 0 of lrt_initialize_devices)
     return render_device(desc, d_backbuffer, d_rays, d_features, (hipStream_t)stream);
 }
 
@@ -2048,20 +2408,23 @@ int lrt_render_host_ex(const lrt_render_desc* desc, float* backbuffer, long long
                        const lrt_features* features) {
     RoctxRange rr_("lrt_render_host_ex");
     std::lock_guard<std::mutex> lk(g_mu);
+    DeviceScope ds_(0);   // context 0's device (device 0 of lrt_initialize_devices)
     return render_host(desc, backbuffer, out_rays, features);
 }
 
 int lrt_render_host(const lrt_render_desc* desc, float* backbuffer, long long* out_rays) {
     RoctxRange rr_("lrt_render_host");
     std::lock_guard<std::mutex> lk(g_mu);
+    DeviceScope ds_(0);   // context 0's device (device 0 of lrt_initialize_devices)
     return render_host(desc, backbuffer, out_rays);
 }
 
 int lrt_stream_create(int reserved_cus, void** out) {
     std::lock_guard<std::mutex> lk(g_mu);
-    if (!g_ctx.ready) return fail(LRT_E_STATE, "lrt_initialize() has not been called");
+    DeviceScope ds_(0);
+    if (!ctx().ready) return fail(LRT_E_STATE, "lrt_initialize() has not been called");
     if (!out) return fail(LRT_E_INVALID, "stream out is NULL");
-    const int n = g_ctx.num_cus;
+    const int n = ctx().num_cus;
     if (reserved_cus < 0 || reserved_cus >= n) return fail(LRT_E_INVALID, "reserved_cus must be in [0, CU count)");
     // the last reserved_cus logical CUs stay free; hipExtStreamCreateWithCUMask takes one
     // bit per CU, 32 per word
@@ -2076,7 +2439,7 @@ int lrt_stream_create(int reserved_cus, void** out) {
     }
     hipStream_t st = nullptr;
     LRT_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
-    g_ctx.masked_streams.emplace_back(st, kept);
+    ctx().masked_streams.emplace_back(st, kept);
     *out = st;
     return LRT_OK;
 }
@@ -2100,7 +2463,7 @@ int lrt_host_free(void* p) {
 
 int lrt_stream_destroy(void* stream) {
     std::lock_guard<std::mutex> lk(g_mu);
-    auto& v = g_ctx.masked_streams;
+    auto& v = ctx().masked_streams;
     for (size_t i = 0; i < v.size(); ++i)
         if (v[i].first == (hipStream_t)stream) {
             (void)hipStreamSynchronize(v[i].first);

@@ -53,8 +53,9 @@ def gather_to_root(local, max_rows: int, world: int, rank: int, gathered=None, g
 
     if local.shape[0] != max_rows:
         raise ValueError("shard buffers must be padded to max_rows rows")
-    if world == 1:
-        return local.unsqueeze(0), None
+    if world == 1 and not dist.is_initialized():
+        return local.unsqueeze(0), None   # no process group: nothing to exchange
+    # (a one-rank group takes the collective too, so the RCCL gather is exercised at N = 1)
     stage = local.is_cuda and dist.get_backend(group) == "gloo"
     send = local.cpu() if stage else local
     out: Optional[List] = None

@@ -35,13 +35,67 @@ def ShutdownTest() -> None:
     L.check(L.lib().lrt_shutdown())
 
 
+def InitializeDevices(device_ids: Optional[Sequence[int]] = None, peer_copy: bool = False) -> None:
+    """InitializeTest over several GPUs of this process (lrt_initialize_devices): DrawTest and
+    render_host then split the rows over all of them, gathered into the first by RCCL
+    (device-to-device copies when an id repeats, or with peer_copy). None: every visible GPU."""
+    flags = L.DEV_PEER_COPY if peer_copy else 0
+    if device_ids is None:
+        L.check(L.lib().lrt_initialize_devices(0, None, flags))
+        return
+    ids = (ctypes.c_int * len(device_ids))(*[int(i) for i in device_ids])
+    L.check(L.lib().lrt_initialize_devices(len(device_ids), ctypes.cast(ids, ctypes.c_void_p), flags))
+
+
+def device_count() -> int:
+    return int(L.lib().lrt_device_count())
+
+
+def host_unregister(backbuffer: np.ndarray) -> None:
+    """Drop the library's page-locking of a pageable buffer it registered (DrawTest does this
+    by itself when the array is freed)."""
+    f = _registered.pop(backbuffer.ctypes.data, None)
+    if f is not None:
+        f.detach()
+    rc = L.lib().lrt_host_unregister(backbuffer.ctypes.data_as(ctypes.c_void_p))
+    if rc not in (L.LRT_OK, L.LRT_E_INVALID):
+        L.check(rc)
+
+
 def DrawTest(time: float, frameCount: int, screenWidth: int, screenHeight: int,
              backbuffer: np.ndarray) -> int:
     _check_host_buffer(backbuffer, screenWidth * screenHeight * 4)
     rays = ctypes.c_int(0)
     L.check(L.lib().lrt_draw_test(float(time), int(frameCount), int(screenWidth), int(screenHeight),
                                   backbuffer.ctypes.data_as(ctypes.c_void_p), ctypes.byref(rays)))
+    if L.last_launch().get("host", "").startswith("registered"):
+        _unregister_when_freed(backbuffer)
     return rays.value
+
+
+_registered = {}   # data pointer -> weakref.finalize of the array that owns the memory
+
+
+def _unregister_when_freed(arr: np.ndarray) -> None:
+    """The library page-locked this pageable buffer (lrt_draw_test's registration cache): drop
+    the registration before numpy frees the memory (a freed range must not stay registered)."""
+    import weakref
+    owner = arr
+    while isinstance(owner.base, np.ndarray):
+        owner = owner.base
+    ptr = arr.ctypes.data
+    f = _registered.get(ptr)
+    if f is not None and f.alive:
+        return
+    _registered[ptr] = weakref.finalize(owner, _unregister_ptr, ptr)
+
+
+def _unregister_ptr(ptr: int) -> None:
+    _registered.pop(ptr, None)
+    try:
+        L.lib().lrt_host_unregister(ctypes.c_void_p(ptr))   # LRT_E_INVALID if already dropped
+    except Exception:  # pragma: no cover - interpreter shutdown
+        pass
 
 
 # ---- extended API -----------------------------------------------------------------------

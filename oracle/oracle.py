@@ -13,6 +13,7 @@ from __future__ import annotations
 import ctypes
 import os
 import subprocess
+import time
 
 import numpy as np
 
@@ -89,8 +90,31 @@ def ref(n: int = 9):
         lib.ref_trace.argtypes = [_P, _P, ctypes.c_int, ctypes.c_uint32, _P]
         lib.ref_scatter.argtypes = [ctypes.c_int, _P, _P, ctypes.c_uint32, _P, _P, _P]
         lib.ref_draw_test.argtypes = [ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]
+        lib.ref_initialize_threads.argtypes = [ctypes.c_int]
         _refs[n] = lib
     return _refs[n]
+
+
+def ref_drawtest_rate(width, height, budget_s, threads):
+    """The reference's own DrawTest as main.cpp:165 calls it -- enkiTS over `threads` workers,
+    kMaxDepth 20, the shared racy RNG (parallel.cpp:297-323, maths.cpp:5) -- on successive
+    frames of one buffer for about budget_s. Returns (Mray/s, frames, rays, seconds).
+    The reference's default scene (libref.so) only; output is non-deterministic by design."""
+    r = ref(9)
+    buf = np.zeros(width * height * 4, np.float32)
+    r.ref_initialize_threads(threads)
+    try:
+        rays = frames = 0
+        t0 = time.perf_counter()
+        while True:
+            rays += r.ref_draw_test(0.0, frames, width, height, _ptr(buf))
+            frames += 1
+            dt = time.perf_counter() - t0
+            if dt >= budget_s:
+                break
+    finally:
+        r.ref_shutdown()
+    return rays / dt / 1e6, frames, rays, dt
 
 
 def ref_scene(n: int = 9):
@@ -121,6 +145,13 @@ def default_scene_arrays():
     return s, m
 
 
+def default_threads() -> int:
+    """Worker threads for the restatement: the host share a GPU box gives one GPU (its
+    OMP_NUM_THREADS, 16 there), not every CPU of the machine; all CPUs here."""
+    n = int(os.environ.get("OMP_NUM_THREADS") or 0)
+    return max(1, min(n, os.cpu_count() or 1)) if n > 0 else min(16, os.cpu_count() or 1)
+
+
 def orc_render(width, height, frames=1, depth=8, frame0=0, x0=0, xc=None, y0=0, yc=None,
                spheres=None, mats=None, cam22=None, buf=None, threads=0):
     """Mode P through the C restatement. Returns (buf[yc, xc, 4], rays)."""
@@ -133,6 +164,7 @@ def orc_render(width, height, frames=1, depth=8, frame0=0, x0=0, xc=None, y0=0, 
     if buf is None:
         buf = np.zeros((yc, xc, 4), np.float32)
     cam = None if cam22 is None else np.ascontiguousarray(cam22, np.float32)
+    threads = threads or default_threads()
     rays = orc().orc_render_p(_ptr(spheres), _ptr(mats), len(spheres) // 4, _ptr(cam), width, height,
                               x0, xc, y0, yc, frame0, frames, depth, _ptr(buf), threads)
     return buf, rays
@@ -164,7 +196,8 @@ def orc_render_ex(width, height, frames=1, depth=8, frame0=0, x0=0, xc=None, y0=
                 assert b.dtype == np.float32 and b.flags.c_contiguous and b.size == yc * xc * 4
                 fp[i] = b.ctypes.data
     rays = orc().orc_render_p_ex(_ptr(spheres), _ptr(mats), len(spheres) // 4, _ptr(cam), width, height,
-                                 x0, xc, y0, yc, frame0, frames, depth, flags, _ptr(buf), fp, max_frame, threads)
+                                 x0, xc, y0, yc, frame0, frames, depth, flags, _ptr(buf), fp, max_frame,
+                                 threads or default_threads())
     return buf, rays
 
 

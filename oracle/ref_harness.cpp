@@ -345,6 +345,13 @@ int ref_draw_test(float time, int frameCount, int w, int h, float* buf) {
     return rays;
 }
 void ref_initialize(void) { InitializeTest(); }
+// InitializeTest (parallel.cpp:231-235) with an explicit worker count: the GPU box's host
+// share is 16 cores while the reference asks sysconf for the whole machine's CPUs
+// (enkiTS Threads.h:91-94). Same scheduler, same g_TS, only the thread count is given.
+void ref_initialize_threads(int threads) {
+    g_TS = enkiNewTaskScheduler();
+    enkiInitTaskSchedulerNumThreads(g_TS, (uint32_t)threads);
+}
 void ref_shutdown(void) { ShutdownTest(); }
 
 }  // extern "C"

@@ -26,13 +26,16 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, w, h, rb, frames, depth, outdir):
+def _worker(rank, world, port, w, h, rb, frames, depth, outdir, backend="gloo"):
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
+    if backend == "nccl":   # RCCL: one rank per GPU, so one rank on this 1-GPU box
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world)
     import learnraytracing_amd as lrt
     from learnraytracing_amd.dist import gather_to_root, max_shard_rows
     from learnraytracing_amd.renderer import pack_rgb_tensor, unshard_rgb_tensor, unshard_tensor
@@ -49,8 +52,9 @@ def _worker(rank, world, port, w, h, rb, frames, depth, outdir):
         torch.cuda.synchronize()
         gathered, _ = gather_to_root(local, max_rows, world, rank)       # RGBA exchange
         gathered3, _ = gather_to_root(packed, max_rows, world, rank)     # RGB exchange (bench.py's)
-        tot = rays.cpu()
+        tot = rays.clone() if backend == "nccl" else rays.cpu()   # RCCL reduces device tensors
         dist.all_reduce(tot)
+        tot = tot.cpu()
         if rank == 0:
             frame = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
             unshard_tensor(gathered, frame, w, h, rb, world)
@@ -78,6 +82,23 @@ def test_two_rank_gpu_shards_assemble_bitwise(gpu, tmp_path, world, rb, frames):
     assert np.array_equal(frame[..., :3].view(np.uint32), want[..., :3].view(np.uint32))
     assert np.array_equal(frame3[..., :3].view(np.uint32), want[..., :3].view(np.uint32))
     assert np.all(frame3[..., 3] == 0.5)   # the RGB exchange leaves the frame's alpha alone
+    assert int(np.load(tmp_path / "rays.npy")[0]) == want_rays
+
+
+def test_one_rank_rccl_gather_assembles_bitwise(gpu, tmp_path):
+    """The RCCL path itself: a one-rank "nccl" (RCCL) process group, where gather_to_root
+    still issues dist.gather (RCCL moves the device shard into rank 0's gathered buffer),
+    then the unshard kernels assemble the frame: bit-identical to a plain render."""
+    import torch.multiprocessing as mp
+    w, h, rb, frames, depth = 256, 144, 8, 4, 8
+    mp.start_processes(_worker, args=(1, _free_port(), w, h, rb, frames, depth, str(tmp_path), "nccl"),
+                       nprocs=1, start_method="spawn", join=True)
+    frame = np.load(tmp_path / "frame.npy")
+    frame3 = np.load(tmp_path / "frame3.npy")
+    want = np.zeros((h, w, 4), np.float32)
+    want_rays = gpu.render_host(gpu.Job(width=w, height=h, frames=frames, max_depth=depth), want)
+    assert np.array_equal(frame[..., :3].view(np.uint32), want[..., :3].view(np.uint32))
+    assert np.array_equal(frame3[..., :3].view(np.uint32), want[..., :3].view(np.uint32))
     assert int(np.load(tmp_path / "rays.npy")[0]) == want_rays
 
 

@@ -32,7 +32,7 @@ def _job(gpu, w, h, frames, depth, frame0=0, flags=0, x0=0, xc=None, y0=0, yc=No
                    row_count=yc, flags=flags)
 
 
-@pytest.mark.parametrize("kernel", [0, 128, 256], ids=["v0", "v3", "wavefront"])
+@pytest.mark.parametrize("kernel", [0, 256, 512], ids=["auto", "wavefront", "pool"])
 @pytest.mark.parametrize("w,h,frames,depth", [(160, 90, 4, 8), (96, 54, 2, 50), (128, 72, 3, 20)])
 def test_no_double_light_vs_oracle(gpu, w, h, frames, depth, kernel):
     buf = np.zeros((h, w, 4), np.float32)
@@ -100,9 +100,9 @@ def test_modes_need_v0(gpu):
     from learnraytracing_amd import _lib as L
     buf = np.zeros((36, 64, 4), np.float32)
     with pytest.raises(LrtError):
-        gpu.render_host_features(_job(gpu, 64, 36, 2, 8, flags=L.F_V3), buf, {"normal": buf.copy()})
+        gpu.render_host_features(_job(gpu, 64, 36, 2, 8, flags=L.F_POOL), buf, {"normal": buf.copy()})
     with pytest.raises(LrtError):
         gpu.render_host_features(_job(gpu, 64, 36, 2, 8, flags=L.F_WAVEFRONT), buf, {"normal": buf.copy()})
-    for removed in (L.F_V1, L.F_V2S, L.F_V2):   # round-1 kernels, removed: rejected loudly
+    for removed in (L.F_V1, L.F_V2S, L.F_V2, L.F_V3):   # removed kernels: rejected loudly
         with pytest.raises(LrtError):
             gpu.render_host(_job(gpu, 64, 36, 2, 8, flags=removed), buf)

@@ -1,0 +1,236 @@
+"""GPU tests of round 3's host-side additions, through the C-ABI:
+
+* lrt_initialize_devices: one process splits a host render over several devices
+  (row-block-cyclic) and gathers the shards into the first -- by RCCL (ncclCommInitAll +
+  grouped ncclGather, rccl.h:745) when the ids are distinct, by device-to-device copies when an
+  id repeats. On a one-GPU box RCCL runs with one device; the copy exchange rehearses 2-3
+  shards on GPU 0. Every frame must equal the one-device render / the oracle bit for bit
+  (parallel.cpp:262,280-286 per pixel; the reference's dispatch over rows, :317-320).
+* the registration cache: a pageable DrawTest buffer (main.cpp:40's `new float[]`) is
+  page-locked on its second call and takes the pinned pipeline, same bits.
+* the pool kernel's heaviest-first tile order on two streams at once (the bench's
+  pipelining), on the exact benchmarked state (order=2), for a new camera (borrowed order),
+  and on the full config-3 frame.
+"""
+import contextlib
+
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _bitwise(got, want, what):
+    g = got[..., :3]
+    w = np.ascontiguousarray(want[..., :3])
+    if not np.array_equal(g.view(np.uint32), w.view(np.uint32)):
+        d = np.abs(g.astype(np.float64) - w.astype(np.float64))
+        raise AssertionError(f"{what}: {int((g != w).any(axis=-1).sum())} pixels differ, max |diff| {d.max():.3g}")
+
+
+@contextlib.contextmanager
+def devices(gpu, ids, peer_copy=False):
+    """Re-initialise the library over `ids` for the block, then back to lrt_initialize."""
+    gpu.ShutdownTest()
+    try:
+        gpu.InitializeDevices(ids, peer_copy=peer_copy)
+        yield
+    finally:
+        gpu.ShutdownTest()
+        gpu.InitializeTest()
+
+
+def _host(gpu, job, buf=None):
+    d = job.desc()
+    if buf is None:
+        buf = np.zeros((d.row_count, d.x_count, 4), np.float32)
+    rays = gpu.render_host(job, buf)
+    return buf, rays
+
+
+@pytest.mark.parametrize("ids,peer,exchange", [([0], False, "rccl"), ([0], True, "copy"), ([0, 0], False, "copy"),
+                                               ([0, 0, 0], False, "copy")],
+                         ids=["rccl-1", "copy-1", "copy-2", "copy-3"])
+def test_multidevice_render_host_equals_oracle(gpu, ids, peer, exchange):
+    from learnraytracing_amd import _lib as L
+    w, h, frames, depth = 320, 180, 4, 8
+    want, wrays = oracle.orc_render(w, h, frames, depth)
+    prev = np.random.default_rng(1).uniform(0, 1, (h, w, 4)).astype(np.float32)
+    want_prev, _ = oracle.orc_render(w, h, frames, depth, frame0=3, buf=prev.copy())
+    with devices(gpu, ids, peer):
+        assert gpu.device_count() == len(ids)
+        buf, rays = _host(gpu, gpu.Job(width=w, height=h, frames=frames, max_depth=depth))
+        info = L.last_launch()
+        assert info["devices"] == str(len(ids)) and info["exchange"] == exchange, info
+        _bitwise(buf, want, f"{len(ids)} devices ({exchange})")
+        assert rays == wrays
+        # progressive: the previous values of every shard come from the caller's buffer;
+        # alpha is carried through the exchange untouched
+        b2 = prev.copy()
+        _host(gpu, gpu.Job(width=w, height=h, frame0=3, frames=frames, max_depth=depth), b2)
+        _bitwise(b2, want_prev, "progressive multi-device")
+        assert np.array_equal(b2[..., 3].view(np.uint32), prev[..., 3].view(np.uint32))
+
+
+@pytest.mark.parametrize("ids", [[0], [0, 0, 0]], ids=["rccl-1", "copy-3"])
+def test_multidevice_drawtest_window_bvh(gpu, ids):
+    """DrawTest (kMaxDepth 20) progressively, a window with odd sizes, and a BVH scene
+    rendered over the devices: all equal the oracle."""
+    from learnraytracing_amd.scene import random_scene, scene_arrays
+    w, h = 200, 120
+    want = np.zeros((h, w, 4), np.float32)
+    for f in range(2):
+        oracle.orc_render(w, h, 1, 20, frame0=f, buf=want)
+    wwin, wwr = oracle.orc_render(97, 61, 3, 8, x0=5, xc=83, y0=7, yc=41)
+    sph, mat = random_scene(300, 4)
+    s, m = (np.array(v, np.float32) for v in scene_arrays(sph, mat))
+    wbvh, wbr = oracle.orc_render(160, 90, 5, 8, spheres=s, mats=m)
+    with devices(gpu, ids):
+        bb = np.zeros(w * h * 4, np.float32)
+        for f in range(2):
+            assert gpu.DrawTest(0.0, f, w, h, bb) > 0
+        _bitwise(bb.reshape(h, w, 4), want, "multi-device DrawTest")
+        win, wr = _host(gpu, gpu.Job(width=97, height=61, frames=3, max_depth=8, x0=5, x_count=83, y0=7, row_count=41))
+        _bitwise(win, wwin, "multi-device window")
+        assert wr == wwr
+        gpu.set_scene(sph, mat)   # every device gets the scene
+        img, r = _host(gpu, gpu.Job(width=160, height=90, frames=5, max_depth=8))
+        _bitwise(img, wbvh, "multi-device BVH scene")
+        assert r == wbr
+
+
+def test_multidevice_caller_shard_stays_on_first_device(gpu):
+    """A caller's own row-block-cyclic shard (row_period > 1) is not split again: device 0
+    renders it, same rows as the oracle."""
+    from learnraytracing_amd import _lib as L
+    w, h, rb, period, phase = 160, 90, 8, 3, 2
+    rows = [y for y in range(h) if (y // rb) % period == phase]
+    want, _ = oracle.orc_render(w, h, 2, 8)
+    with devices(gpu, [0, 0]):
+        buf, _ = _host(gpu, gpu.Job(width=w, height=h, frames=2, max_depth=8, row_block=rb, row_period=period,
+                                    row_phase=phase))
+        assert "devices" not in L.last_launch()
+    _bitwise(buf, want[rows], "caller shard")
+
+
+def test_initialize_devices_validation(gpu):
+    from learnraytracing_amd import _lib as L
+    with pytest.raises(L.LrtError):          # already initialised (the session's lrt_initialize)
+        gpu.InitializeDevices([0])
+    gpu.ShutdownTest()
+    try:
+        for bad in ([99], [-1]):
+            with pytest.raises(L.LrtError):
+                gpu.InitializeDevices(bad)
+        assert gpu.device_count() == 0
+    finally:
+        gpu.InitializeTest()
+    assert gpu.device_count() == 1
+
+
+def test_pageable_drawtest_buffer_is_registered(gpu):
+    """main.cpp's pattern: one pageable buffer for every frame. The first call stages it, the
+    second registers it (host=registered-pipelined) -- same bits as the oracle's frames."""
+    from learnraytracing_amd import _lib as L
+    w, h = 320, 180
+    gpu.DrawTest(0.0, 0, 8, 8, np.zeros(8 * 8 * 4, np.float32))   # the cache's "last buffer" is another one
+    bb = np.zeros(w * h * 4, np.float32)
+    want = np.zeros((h, w, 4), np.float32)
+    paths = []
+    try:
+        for f in range(4):
+            gpu.DrawTest(0.0, f, w, h, bb)
+            paths.append(L.last_launch().get("host"))
+            oracle.orc_render(w, h, 1, 20, frame0=f, buf=want)
+    finally:
+        gpu.host_unregister(bb)
+    assert paths[0] == "staged" and paths[1:] == ["registered-pipelined"] * 3, paths
+    _bitwise(bb.reshape(h, w, 4), want, "registered DrawTest")
+    # unregistered again: the next call stages (and a fresh buffer is not registered at once)
+    gpu.DrawTest(0.0, 4, w, h, bb)
+    assert L.last_launch()["host"] == "staged"
+
+
+def _torch_render(gpu, job, stream, out):
+    import torch
+    rays = torch.zeros(1, dtype=torch.int64, device="cuda")
+    gpu.render_tensor(job, out, rays, stream)
+    return rays
+
+
+def test_pool_order_two_streams_bitwise(gpu):
+    """The bench's pipelining: config 2 launched alternately on two streams, each into its own
+    buffer, across the recording launch and the switch to the heaviest-first order. Every
+    frame equals the single-stream render (the order is uploaded before any stream reads it)."""
+    import torch
+    from learnraytracing_amd import _lib as L
+    w, h = 1280, 720
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = [torch.zeros((h, w, 4), dtype=torch.float32, device="cuda") for _ in range(8)]
+    orders = []
+    cam = gpu.make_camera((0.1, 2, 3), (0, 0, 0), (0, 1, 0), 60, w / h, 0.1, 3)   # a signature of its own
+    job2 = gpu.Job(width=w, height=h, frames=4, max_depth=8, camera=cam)
+    for k, o in enumerate(outs):
+        _torch_render(gpu, job2, streams[k % 2], o)
+        orders.append(L.last_launch()["order"])
+        if k == 0:
+            torch.cuda.synchronize()   # the recording launch ends: launch 1 sorts and uploads the order
+    torch.cuda.synchronize()
+    want, _ = oracle.orc_render(w, h, 4, 8, cam22=cam.to22())
+    for k, o in enumerate(outs):
+        _bitwise(o.cpu().numpy(), want, f"launch {k} (order {orders[k]})")
+    assert orders[0] in ("1", "3") and orders[1:] == ["2"] * 7, orders
+
+
+def test_config2_benchmarked_state_vs_oracle(gpu):
+    """The exact state bench.py times: config 2 through lrt_render_device after a recording
+    launch, i.e. pool_kernel with the heaviest-first order (order=2), full frame, bit-exact."""
+    import torch
+    from learnraytracing_amd import _lib as L
+    w, h = 1280, 720
+    job = gpu.Job(width=w, height=h, frames=4, max_depth=8)
+    s = torch.cuda.current_stream()
+    warm = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
+    _torch_render(gpu, job, s, warm)
+    torch.cuda.synchronize()
+    out = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
+    rays = _torch_render(gpu, job, s, out)
+    info = L.last_launch()
+    assert info["kernel"] == "pool_kernel" and info["order"] == "2" and info["ns"] == "9", info
+    torch.cuda.synchronize()
+    want, wrays = oracle.orc_render(w, h, 4, 8)
+    _bitwise(out.cpu().numpy(), want, "config 2, order=2")
+    assert int(rays.item()) == wrays == 11669343
+
+
+def test_new_view_borrows_order_bitwise(gpu):
+    """A camera move keeps the geometry: its first launch borrows the previous view's ready
+    order (order=3) instead of running in queue order; the pixels are the new view's."""
+    from learnraytracing_amd import _lib as L
+    w, h = 1280, 720
+    for _ in range(2):   # view A: recording launch, then its own order
+        _host(gpu, gpu.Job(width=w, height=h, frames=4, max_depth=8))
+    assert L.last_launch()["order"] == "2"
+    cam = gpu.make_camera((0.3, 2.1, 3), (0, 0, 0), (0, 1, 0), 60, w / h, 0.1, 3)
+    buf, rays = _host(gpu, gpu.Job(width=w, height=h, frames=4, max_depth=8, camera=cam))
+    assert L.last_launch()["order"] == "3"
+    want, wrays = oracle.orc_render(w, h, 4, 8, cam22=cam.to22())
+    _bitwise(buf, want, "moved camera, borrowed order")
+    assert rays == wrays
+
+
+def test_config3_full_frame_vs_oracle(gpu):
+    """BASELINE config 3 at full size (1920x1080, 16 spp, 50 bounces, ~106 M rays) on the
+    instance and order the benchmark runs (pool kernel, heaviest-first after a recording
+    launch): bit-exact vs the C oracle."""
+    from learnraytracing_amd import _lib as L
+    job = gpu.Job(width=1920, height=1080, frames=16, max_depth=50)
+    _host(gpu, job)
+    buf, rays = _host(gpu, job)
+    info = L.last_launch()
+    assert info["kernel"] == "pool_kernel" and info["maxd"] == "64" and info["order"] == "2", info
+    want, wrays = oracle.orc_render(1920, 1080, 16, 50)
+    _bitwise(buf, want, "config 3 full frame")
+    assert rays == wrays

@@ -41,11 +41,11 @@ def test_golden_mode_p(gpu, manifest, images, name):
     assert rays == fx["rays"]
 
 
-@pytest.mark.parametrize("flags", [0, 1, 2, 3, 128, 129, 256, 257, 512, 513])
+@pytest.mark.parametrize("flags", [0, 1, 2, 3, 256, 257, 512, 513])
 @pytest.mark.parametrize("name", ["p_160x90_s4_d8", "p_96x54_s1_d50"])
 def test_golden_kernel_variants(gpu, manifest, images, flags, name):
-    """Every kernel (v0 default / LRT_F_SIMPLE, v3 LRT_F_V3, v4 LRT_F_WAVEFRONT), with
-    LDS-staged or global scene reads, gives the same bits."""
+    """Every kernel (the policy's pick, v0 LRT_F_SIMPLE, v4 LRT_F_WAVEFRONT, v5 LRT_F_POOL),
+    with LDS-staged or global scene reads, gives the same bits."""
     fx = manifest["fixtures"][name]
     buf, rays = _render(gpu, fx["w"], fx["h"], fx["frames"], fx["max_depth"], flags=flags)
     _assert_bitwise(buf, images[name], f"{name} flags={flags}")
@@ -148,11 +148,11 @@ def test_host_alloc_backbuffer(gpu):
         assert gpu.lib().lrt_host_free(p) == 0
 
 
-@pytest.mark.parametrize("kflags,frames", [(0, 6), (0, 40), (128, 6)], ids=["v0", "v0-samples", "v3"])
+@pytest.mark.parametrize("kflags,frames", [(0, 6), (0, 40), (256, 6)], ids=["v0", "v0-samples", "wavefront"])
 def test_render_host_pinned_window(gpu, kflags, frames):
     """lrt_render_host on a pinned buffer: a window of 37 rows x 90 columns equals the
     pageable call bit for bit (and so the one-launch render), alpha included; v0 (also with
-    many frames, sample mode's merge) and v3 (which stages instead)."""
+    many frames, sample mode's merge) and the wavefront kernels (which stage instead)."""
     job = gpu.Job(width=160, height=90, frames=frames, max_depth=8, x0=30, x_count=90, y0=40, row_count=37,
                   flags=kflags)
     a = np.random.default_rng(3).uniform(0, 1, 37 * 90 * 4).astype(np.float32)
@@ -294,7 +294,7 @@ def test_deterministic_repeat_full_config2(gpu):
 
 
 @pytest.mark.parametrize("n,seed", [(17, 3), (200, 5), (1000, 1), (4096, 7)])
-@pytest.mark.parametrize("kflags", [2, 128, 256, 512])
+@pytest.mark.parametrize("kflags", [2, 256, 512])
 def test_bvh_equals_linear_scan(gpu, n, seed, kflags):
     """The BVH closest hit returns the reference's scan result bit for bit: same
     pixels and ray counts as LRT_F_NO_BVH, for every kernel."""
@@ -369,19 +369,27 @@ def test_cu_reserved_render_stream(gpu):
             rs.close()
 
 
-V3 = 128   # LRT_F_V3: path regeneration inside the wave
+V0 = 2     # LRT_F_SIMPLE: the per-pixel loop, frames over lanes
 WF = 256   # LRT_F_WAVEFRONT: breadth-first kernels over compacted queues
 POOL = 512   # LRT_F_POOL: sample-pool regeneration inside the wave
-ALT = pytest.mark.parametrize("kflags", [V3, WF, POOL], ids=["v3", "wavefront", "pool"])
+ALT = pytest.mark.parametrize("kflags", [V0, WF, POOL], ids=["v0", "wavefront", "pool"])
 
 
 @ALT
-def test_v3_config2_full_frame_vs_oracle(gpu, kflags):
-    """v3 and the wavefront kernels on BASELINE config 2 at full size, bit-exact vs the C oracle."""
+def test_kernel_config2_full_frame_vs_oracle(gpu, kflags):
+    """Each kernel forced on BASELINE config 2 at full size, bit-exact vs the C oracle."""
     buf, rays = _render(gpu, 1280, 720, 4, 8, flags=kflags)
     want, wrays = oracle.orc_render(1280, 720, 4, 8)
-    _assert_bitwise(buf, want[..., :3], "v3 config2 full frame")
+    _assert_bitwise(buf, want[..., :3], f"flags={kflags} config2 full frame")
     assert rays == wrays
+
+
+def test_v3_flag_is_rejected(gpu):
+    """Round 3 removed v3 (LRT_F_V3): the flag fails loudly instead of running another kernel."""
+    from learnraytracing_amd import _lib as L
+    with pytest.raises(L.LrtError) as e:
+        _render(gpu, 16, 8, 1, 8, flags=L.F_V3)
+    assert e.value.code == L.LRT_E_INVALID
 
 
 @pytest.mark.parametrize("case", [
@@ -391,17 +399,17 @@ def test_v3_config2_full_frame_vs_oracle(gpu, kflags):
     (33, 9, 1, 8, 0, 0, None, 0, None),        # fewer pixels than one wave per queue
 ])
 @ALT
-def test_v3_windows_vs_oracle(gpu, case, kflags):
+def test_kernel_windows_vs_oracle(gpu, case, kflags):
     w, h, frames, depth, f0, x0, xc, y0, yc = case
     buf, rays = _render(gpu, w, h, frames, depth, frame0=f0, x0=x0, xc=xc, y0=y0, yc=yc, flags=kflags)
     want, wrays = oracle.orc_render(w, h, frames, depth, frame0=f0, x0=x0, xc=xc, y0=y0, yc=yc)
-    _assert_bitwise(buf, want[..., :3], f"v3 {case}")
+    _assert_bitwise(buf, want[..., :3], f"flags={kflags} {case}")
     assert rays == wrays
 
 
 @ALT
-def test_v3_fuzz_and_scene1000(gpu, manifest, images, kflags):
-    """v3 on the fuzzed scenes (all materials, TIR, 1-3 lights) and the 1000-sphere crops."""
+def test_kernel_fuzz_and_scene1000(gpu, manifest, images, kflags):
+    """Each kernel on the fuzzed scenes (all materials, TIR, 1-3 lights) and the 1000-sphere crops."""
     from learnraytracing_amd import _lib as L
     from learnraytracing_amd.scene import scene_from_arrays
     try:
@@ -414,22 +422,22 @@ def test_v3_fuzz_and_scene1000(gpu, manifest, images, kflags):
                 setattr(cam, n, L.f3(*vals[3 * i:3 * i + 3]))
             cam.lensRadius = vals[21]
             buf, rays = _render(gpu, fz["w"], fz["h"], fz["frames"], fz["max_depth"], camera=cam, flags=kflags)
-            _assert_bitwise(buf, images[fz["name"]], "v3 " + fz["name"])
+            _assert_bitwise(buf, images[fz["name"]], f"flags={kflags} " + fz["name"])
             assert rays == fz["rays"], fz["name"]
         gpu.set_scene(*gpu.random_scene(1000, 1))
         for name in ("scene1000_c4_crop", "scene1000_c5_crop"):
             fx = manifest["fixtures"][name]
             buf, rays = _render(gpu, fx["w"], fx["h"], fx["frames"], fx["max_depth"], 0, fx["x0"], fx["xc"],
                                 fx["y0"], fx["yc"], flags=kflags)
-            _assert_bitwise(buf, images[name], "v3 " + name)
+            _assert_bitwise(buf, images[name], f"flags={kflags} " + name)
             assert rays == fx["rays"]
     finally:
         gpu.set_scene(*gpu.default_scene())
 
 
 @ALT
-def test_v3_row_block_cyclic_shard(gpu, kflags):
-    """A v3 shard (rows dealt in blocks of 8 over 3 ranks, rank 1) equals the oracle's rows."""
+def test_kernel_row_block_cyclic_shard(gpu, kflags):
+    """A shard (rows dealt in blocks of 8 over 3 ranks, rank 1) equals the oracle's rows."""
     w, h, rb, period, phase = 320, 180, 8, 3, 1
     rows = [y for y in range(h) if (y // rb) % period == phase]
     job = gpu.Job(width=w, height=h, frames=2, max_depth=8, row_block=rb, row_period=period, row_phase=phase,
@@ -437,7 +445,7 @@ def test_v3_row_block_cyclic_shard(gpu, kflags):
     buf = np.zeros((len(rows), w, 4), np.float32)
     rays = gpu.render_host(job, buf)
     want, wrays = oracle.orc_render(w, h, 2, 8)
-    _assert_bitwise(buf, want[rows][..., :3], "v3 shard")
+    _assert_bitwise(buf, want[rows][..., :3], f"flags={kflags} shard")
     assert rays == sum(oracle.orc_render(w, h, 2, 8, y0=y, yc=1)[1] for y in rows)
 
 
@@ -482,7 +490,7 @@ EDGE_CASES = {
 }
 
 
-@pytest.mark.parametrize("kflags", [0, V3, WF, POOL], ids=["auto", "v3", "wavefront", "pool"])
+@pytest.mark.parametrize("kflags", [0, V0, WF, POOL], ids=["auto", "v0", "wavefront", "pool"])
 @pytest.mark.parametrize("case", list(EDGE_CASES), ids=list(EDGE_CASES))
 def test_edge_cases_vs_oracle(gpu, case, kflags):
     """Degenerate sizes, depth budgets 0/1/64, frame numbers at the lerp table's end and
