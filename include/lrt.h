@@ -273,10 +273,12 @@ int lrt_libm_eval_host(int kind, const float* in, float* out, long long n);
 int lrt_libm_eval_device(int kind, const float* d_in, float* d_out, long long n);
 
 /* BVH diagnostics (host only, no GPU): build the BVH of the given scene and trace n rays
- * (6 floats each: origin, direction) with the device traversal code. out[5]: mean nodes
- * visited, mean spheres tested, max nodes, max spheres, and mismatches per ray against
- * the linear scan (0 by construction): closest hit (id and t), and the bounded shadow-ray
- * traversal for the scan's winner and for one other sphere per ray. */
+ * (6 floats each: origin, direction) with the device traversal code. out[7]: mean nodes
+ * visited, mean spheres tested, max nodes, max spheres, mismatches per ray against the
+ * linear scan (0 by construction: closest hit (id and t), the bounded shadow-ray traversal
+ * for the scan's winner and for one other sphere per ray, the two-query loop), the deepest
+ * traversal-stack entry any of those traversals wrote, and the entries the device's LDS
+ * stack holds for this scene (the first must not exceed the second). */
 int lrt_bvh_stats(const lrt_sphere* spheres, int count, const float* rays, int n, double* out);
 /* Closest hit of n rays (6 floats each; d normalised as the Ray ctor does) through the BVH
  * of the given scene: ids[i] (-1: miss) and ts[i]. mode 0: host build of the per-lane

@@ -56,9 +56,6 @@ LRT_DEV void SlabTest(const float4& mn, const float4& mx, const F3& o, const F3&
 // instead of a subtract and a multiply. Beyond the subtract-multiply form's rounding it
 // errs by at most ulp(|o_k * inv_k|) per plane; MakeSlabRay bounds that once per ray
 // and the culling margins add it, so culling stays conservative.
-#ifndef LRT_BVH_FMA_SLAB
-#define LRT_BVH_FMA_SLAB 1
-#endif
 LRT_DEV void SlabTestFma(const float4& mn, const float4& mx, const F3& inv, const F3& oi, float& tn, float& tf) {
     const float tx0 = __builtin_fmaf(mn.x, inv.x, -oi.x), tx1 = __builtin_fmaf(mx.x, inv.x, -oi.x);
     const float ty0 = __builtin_fmaf(mn.y, inv.y, -oi.y), ty1 = __builtin_fmaf(mx.y, inv.y, -oi.y);
@@ -86,7 +83,7 @@ LRT_DEV SlabRay MakeSlabRay(const F3& o, const F3& d, float margin) {
     const float mo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(o.x), __builtin_fabsf(o.y)), __builtin_fabsf(o.z));
     // margin = 1e-5 * extent + 1e-4 (build_bvh_host): every box coordinate is below 1e5 * margin
     const float bound = mi * (1.0e5f * margin + mo);
-    r.fma = LRT_BVH_FMA_SLAB && bound < 1.0e30f;   // false for inf / NaN too
+    r.fma = bound < 1.0e30f;   // false for inf / NaN too
     r.mo = r.fma ? __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.oi.x), __builtin_fabsf(r.oi.y)),
                                    __builtin_fabsf(r.oi.z)) * 2.384185791015625e-07f
                  : 0.0f;
@@ -97,214 +94,41 @@ LRT_DEV void SlabTest4(const float4& mn, const float4& mx, const F3& o, const Sl
     else SlabTest(mn, mx, o, sr.inv, tn, tf);
 }
 
-struct BvhStats { int nodes = 0, spheres = 0; };   // host diagnostics (lrt_bvh_stats)
+// Host diagnostics (lrt_bvh_stats): node visits, sphere tests and the deepest traversal
+// stack entry written, checked against the levels the LDS stack is sized to.
+struct BvhStats { int nodes = 0, spheres = 0, max_sp = 0; };
 
-// LRT_BVH4 (default): the BVH2 collapsed to 4-wide nodes (8 float4: four children's boxes,
-// same per-child encoding; empty slots have count -1). Half the levels, so fewer and
-// fuller traversal iterations. A stack entry is (node << 4 | mask of the node's children
-// still to visit), one entry per level. A popped entry descends into its first child
-// without a second box test: every pushed child already passed the cull against a bound
-// that has only shrunk since, so skipping the re-test is conservative.
-#ifndef LRT_BVH4
-#define LRT_BVH4 1
-#endif
-// LRT_BVH_PRELOAD: a node's 8 float4 are loaded at the top of the iteration, in one round
-// trip, instead of each child's pair after the previous child's box and leaf tests.
-#ifndef LRT_BVH_PRELOAD
-#define LRT_BVH_PRELOAD 0
-#endif
-#ifndef LRT_BVH_CH_RETEST   // closest hit: re-test popped children against the shrunk bestT (A/B)
-#define LRT_BVH_CH_RETEST 0
-#endif
-// A BVH4 stack entry is a u16 (node << 4 | mask): node indices must stay below 4096. The
-// 4-wide node count is at most the BVH2's internal node count, < LRT_MAX_SPHERES.
+// The BVH2 the host builds is collapsed to 4-wide nodes (8 float4: four children's boxes,
+// per-child encoding as above; empty slots have count -1). A stack entry is a u16 (node << 4
+// | mask of the node's children still to visit), one entry per level: a push happens only
+// when descending from a node to an internal child, so the stack never holds more entries
+// than the tree's depth (BvhHost::stack_levels, which sizes the LDS stack). A popped entry
+// descends into its first child without a second box test: every pushed child already
+// passed the cull against a bound that has only shrunk since, so skipping the re-test is
+// conservative. Node indices must stay below 4096 (12 bits).
 static_assert(LRT_MAX_SPHERES <= 4096, "BVH4 stack entries hold 12-bit node indices");
 
-// stk: this lane's traversal stack (kBvhStackLevels entries, stride `stride`).
-LRT_DEV int ClosestHitBVH2(const F3& o, const F3& d, const BvhView& bv, float& tOut, unsigned short* stk,
-                          int stride, BvhStats* st = nullptr) {
-    const F3 inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    float bestT = kMaxT;
-    int best = -1;
-    int sp = 0, cur = 0;
-    auto leaf = [&](int ref, int cnt) {
-        if (st) st->spheres += cnt;
-        for (int j = 0; j < cnt; ++j) {
-            const float4 s = bv.lsph[ref + j];
-            const F3 rs = f3(s.x, s.y, s.z) - o;                       // maths.cpp:54-59
-            const float rsProj = dot(rs, d);
-            const float ifHit = dot(rs, rs) - rsProj * rsProj - s.w;
-            if (ifHit < 0.0f) {
-                const float halfCut = sqrt_rn(-ifHit);
-                const float t1 = rsProj - halfCut;
-                const float t2 = rsProj + halfCut;
-                const float cand = t1 > kMinT ? t1 : (t2 > kMinT ? t2 : __builtin_inff());
-                const int id = bv.lid[ref + j];
-                if (cand < bestT || (cand == bestT && best >= 0 && id < best)) {
-                    bestT = cand;
-                    best = id;
-                }
-            }
-        }
-    };
-    leaf(bv.big0, bv.nbig);   // seeds bestT, which then culls the traversal
-    if (bv.nnodes == 0) {
-        tOut = bestT;
-        return best;
-    }
-    for (;;) {
-        const float4 a0 = bv.nodes[4 * cur + 0], a1 = bv.nodes[4 * cur + 1];
-        const float4 b0 = bv.nodes[4 * cur + 2], b1 = bv.nodes[4 * cur + 3];
-        if (st) st->nodes += 1;
-        float tnA, tfA, tnB, tfB;
-        SlabTest(a0, a1, o, inv, tnA, tfA);
-        SlabTest(b0, b1, o, inv, tnB, tfB);
-        // conservative margins: absolute (scene extent) + relative to the distances compared
-        const float mb = bv.margin + 1e-5f * bestT;
-        const float mA = bv.margin + 1e-5f * __builtin_fabsf(tfA);
-        const float mB = bv.margin + 1e-5f * __builtin_fabsf(tfB);
-        const int cntA = lrt::libm::f2u_i(a1.w), cntB = lrt::libm::f2u_i(b1.w);
-        const bool hitA = cntA >= 0 && tnA <= tfA + mA && tnA <= bestT + mb && tfA >= kMinT - mA;
-        const bool hitB = cntB >= 0 && tnB <= tfB + mB && tnB <= bestT + mb && tfB >= kMinT - mB;
-        if (hitA && cntA > 0) leaf(lrt::libm::f2u_i(a0.w), cntA);
-        if (hitB && cntB > 0) leaf(lrt::libm::f2u_i(b0.w), cntB);
-        const bool goA = hitA && cntA == 0, goB = hitB && cntB == 0;
-        if (goA && goB) {
-            const bool aFirst = tnA <= tnB;
-            stk[sp * stride] = (unsigned short)lrt::libm::f2u_i(aFirst ? b0.w : a0.w);
-            ++sp;
-            cur = lrt::libm::f2u_i(aFirst ? a0.w : b0.w);
-        } else if (goA) {
-            cur = lrt::libm::f2u_i(a0.w);
-        } else if (goB) {
-            cur = lrt::libm::f2u_i(b0.w);
-        } else {
-            if (sp == 0) break;
-            --sp;
-            cur = stk[sp * stride];
-        }
-    }
-    tOut = bestT;
-    return best;
-}
-
-// Light sampling's `HitWorld(shadow ray) && hitID == li` (parallel.cpp:122-123) through
-// the BVH. (cand_li, li) must be the lexicographic minimum, so the light's own candidate
-// is the bar from the start: boxes beyond it are culled (same conservative margins) and
-// the first sphere that beats it -- cand_j < cand_li, or equal with j < li -- ends the
-// traversal. Same per-sphere arithmetic as the scan, so the answer is bit-identical.
-LRT_DEV float SphereCand(const F3& o, const F3& d, const float4& s) {   // maths.cpp:54-90
-    const F3 rs = f3(s.x, s.y, s.z) - o;
-    const float rsProj = dot(rs, d);
-    const float ifHit = dot(rs, rs) - rsProj * rsProj - s.w;
-    if (!(ifHit < 0.0f)) return __builtin_inff();
-    const float halfCut = sqrt_rn(-ifHit);
-    const float t1 = rsProj - halfCut;
-    const float t2 = rsProj + halfCut;
-    return t1 > kMinT ? t1 : (t2 > kMinT ? t2 : __builtin_inff());
-}
-LRT_DEV bool ShadowReachesLightBVH2(const F3& o, const F3& d, int li, const float4& lightSph, const BvhView& bv,
-                                   unsigned short* stk, int stride) {
-    const float candL = SphereCand(o, d, lightSph);
-    if (!(candL < kMaxT)) return false;   // the light is not hit at all (closestT starts at kMaxT)
-    auto beats = [&](float c, int id) { return c < candL || (c == candL && id < li); };
-    for (int j = 0; j < bv.nbig; ++j)
-        if (beats(SphereCand(o, d, bv.lsph[bv.big0 + j]), bv.lid[bv.big0 + j])) return false;
-    if (bv.nnodes == 0) return true;
-    const F3 inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    const float mb = bv.margin + 1e-5f * candL;
-    int sp = 0, cur = 0;
-    for (;;) {
-        const float4 a0 = bv.nodes[4 * cur + 0], a1 = bv.nodes[4 * cur + 1];
-        const float4 b0 = bv.nodes[4 * cur + 2], b1 = bv.nodes[4 * cur + 3];
-        float tnA, tfA, tnB, tfB;
-        SlabTest(a0, a1, o, inv, tnA, tfA);
-        SlabTest(b0, b1, o, inv, tnB, tfB);
-        const float mA = bv.margin + 1e-5f * __builtin_fabsf(tfA);
-        const float mB = bv.margin + 1e-5f * __builtin_fabsf(tfB);
-        const int cntA = lrt::libm::f2u_i(a1.w), cntB = lrt::libm::f2u_i(b1.w);
-        const bool hitA = cntA >= 0 && tnA <= tfA + mA && tnA <= candL + mb && tfA >= kMinT - mA;
-        const bool hitB = cntB >= 0 && tnB <= tfB + mB && tnB <= candL + mb && tfB >= kMinT - mB;
-        if (hitA && cntA > 0) {
-            const int ref = lrt::libm::f2u_i(a0.w);
-            for (int j = 0; j < cntA; ++j)
-                if (beats(SphereCand(o, d, bv.lsph[ref + j]), bv.lid[ref + j])) return false;
-        }
-        if (hitB && cntB > 0) {
-            const int ref = lrt::libm::f2u_i(b0.w);
-            for (int j = 0; j < cntB; ++j)
-                if (beats(SphereCand(o, d, bv.lsph[ref + j]), bv.lid[ref + j])) return false;
-        }
-        const bool goA = hitA && cntA == 0, goB = hitB && cntB == 0;
-        if (goA && goB) {
-            const bool aFirst = tnA <= tnB;
-            stk[sp * stride] = (unsigned short)lrt::libm::f2u_i(aFirst ? b0.w : a0.w);
-            ++sp;
-            cur = lrt::libm::f2u_i(aFirst ? a0.w : b0.w);
-        } else if (goA) {
-            cur = lrt::libm::f2u_i(a0.w);
-        } else if (goB) {
-            cur = lrt::libm::f2u_i(b0.w);
-        } else {
-            if (sp == 0) break;
-            --sp;
-            cur = stk[sp * stride];
-        }
-    }
-    return true;
-}
-
-
-// Traversal knobs (A/B builds; defaults are the measured best):
-//  LRT_BVH_LAZY_ID   the leaf loop keeps the winner's leaf-array position and reads original
-//                    indices only on an exact tie and once at the end (no dependent id load
-//                    per tested sphere);
-//  LRT_BVH_SLAB_SPLIT the traversal loop is instantiated for each slab form and chosen once
-//                    per ray, instead of a (nearly always uniform) branch per child;
-//  LRT_BVH_LEAF_BATCH a leaf's sphere loads (up to kLeafBatch) are issued together before
-//                    the tests, one round trip instead of one per sphere.
-#ifndef LRT_BVH_LAZY_ID
-#define LRT_BVH_LAZY_ID 1
-#endif
-#ifndef LRT_BVH_SLAB_SPLIT
-#define LRT_BVH_SLAB_SPLIT 1
-#endif
-#ifndef LRT_BVH_LEAF_BATCH
-#define LRT_BVH_LEAF_BATCH 0
-#endif
-constexpr int kLeafBatch = 6;   // the build's default leaf size (kBvhLeaf); longer leaves loop on
-
-template <int kForm>   // 0: SlabTest4's runtime choice, 1: FMA form, 2: subtract-multiply form
+template <int kForm>   // 1: FMA slab form, 2: subtract-multiply form (MakeSlabRay chooses per ray)
 LRT_DEV void SlabTestK(const float4& mn, const float4& mx, const F3& o, const SlabRay& sr, float& tn, float& tf) {
     if (kForm == 1) SlabTestFma(mn, mx, sr.inv, sr.oi, tn, tf);
-    else if (kForm == 2) SlabTest(mn, mx, o, sr.inv, tn, tf);
-    else SlabTest4(mn, mx, o, sr, tn, tf);
+    else SlabTest(mn, mx, o, sr.inv, tn, tf);
 }
 
-// Calls f(position, sphere) for the cnt leaf spheres at lsph[ref ...], their loads issued
-// together (LRT_BVH_LEAF_BATCH).
-template <class F>
-LRT_DEV void ForLeafSpheres(const float4* lsph, int ref, int cnt, F&& f) {
-    if (LRT_BVH_LEAF_BATCH) {
-        float4 sb[kLeafBatch];
-#pragma unroll
-        for (int j = 0; j < kLeafBatch; ++j)
-            if (j < cnt) sb[j] = lsph[ref + j];
-#pragma unroll
-        for (int j = 0; j < kLeafBatch; ++j)
-            if (j < cnt) f(ref + j, sb[j]);
-        for (int j = kLeafBatch; j < cnt; ++j) f(ref + j, lsph[ref + j]);
-    } else {
-        for (int j = 0; j < cnt; ++j) f(ref + j, lsph[ref + j]);
-    }
+// Pushes (node, mask) as stack entry sp (host builds track the depth reached).
+LRT_DEV void StackPush(unsigned short* stk, int stride, int& sp, int node, int mask, BvhStats* st) {
+    stk[sp * stride] = (unsigned short)((node << 4) | mask);
+    ++sp;
+    if (st && sp > st->max_sp) st->max_sp = sp;
 }
 
-// 4-wide ClosestHitBVH: same leaf arithmetic, (cand, id) minimum and conservative culling.
+// 4-wide closest hit: the reference's per-sphere arithmetic, the (cand, id) minimum and
+// conservative culling. The winner is kept as its position in lsph; the original index is
+// read only on an exact tie and once at the end.
 template <int kForm>
 LRT_DEV int ClosestHitBVH4Impl(const F3& o, const F3& d, const SlabRay& sr, const BvhView& bv, float& tOut,
                                unsigned short* stk, int stride, BvhStats* st) {
     float bestT = kMaxT;
-    int best = -1;   // LRT_BVH_LAZY_ID: the winner's position in lsph, else its original index
+    int best = -1;
     auto test = [&](int pos, const float4& s) {
         const F3 rs = f3(s.x, s.y, s.z) - o;                       // maths.cpp:54-59
         const float rsProj = dot(rs, d);
@@ -314,23 +138,15 @@ LRT_DEV int ClosestHitBVH4Impl(const F3& o, const F3& d, const SlabRay& sr, cons
             const float t1 = rsProj - halfCut;
             const float t2 = rsProj + halfCut;
             const float cand = t1 > kMinT ? t1 : (t2 > kMinT ? t2 : __builtin_inff());
-            if (LRT_BVH_LAZY_ID) {
-                if (cand < bestT || (cand == bestT && best >= 0 && bv.lid[pos] < bv.lid[best])) {
-                    bestT = cand;
-                    best = pos;
-                }
-            } else {
-                const int id = bv.lid[pos];
-                if (cand < bestT || (cand == bestT && best >= 0 && id < best)) {
-                    bestT = cand;
-                    best = id;
-                }
+            if (cand < bestT || (cand == bestT && best >= 0 && bv.lid[pos] < bv.lid[best])) {
+                bestT = cand;
+                best = pos;
             }
         }
     };
     auto leaf = [&](int ref, int cnt) {
         if (st) st->spheres += cnt;
-        ForLeafSpheres(bv.lsph, ref, cnt, test);
+        for (int j = 0; j < cnt; ++j) test(ref + j, bv.lsph[ref + j]);
     };
     leaf(bv.big0, bv.nbig);
     int sp = 0, cur = 0, msk = bv.nnodes == 0 ? 0 : 0xF;
@@ -340,16 +156,11 @@ LRT_DEV int ClosestHitBVH4Impl(const F3& o, const F3& d, const SlabRay& sr, cons
         const float mbase = bv.margin + sr.mo;
         int next = -1, rem = 0, nextRef = 0;
         float nearT = __builtin_inff();
-        float4 nd[8];
-        if (LRT_BVH_PRELOAD) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) nd[k] = bv.nodes[8 * cur + k];
-        }
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             if (!((msk >> c) & 1)) continue;
-            const float4 lo = LRT_BVH_PRELOAD ? nd[2 * c] : bv.nodes[8 * cur + 2 * c];
-            const float4 hi = LRT_BVH_PRELOAD ? nd[2 * c + 1] : bv.nodes[8 * cur + 2 * c + 1];
+            const float4 lo = bv.nodes[8 * cur + 2 * c];
+            const float4 hi = bv.nodes[8 * cur + 2 * c + 1];
             const int cnt = lrt::libm::f2u_i(hi.w);
             if (cnt < 0) continue;
             float tn, tf;
@@ -370,10 +181,7 @@ LRT_DEV int ClosestHitBVH4Impl(const F3& o, const F3& d, const SlabRay& sr, cons
         }
         if (next >= 0) {
             rem &= ~(1 << next);
-            if (rem) {
-                stk[sp * stride] = (unsigned short)((cur << 4) | rem);
-                ++sp;
-            }
+            if (rem) StackPush(stk, stride, sp, cur, rem, st);
             cur = nextRef;
             msk = 0xF;
         } else {
@@ -382,37 +190,44 @@ LRT_DEV int ClosestHitBVH4Impl(const F3& o, const F3& d, const SlabRay& sr, cons
             const int e = stk[sp * stride];
             cur = e >> 4;
             msk = e & 0xF;
-#if !LRT_BVH_CH_RETEST
             const int c = __builtin_ctz(msk);
             msk &= msk - 1;
-            if (msk) {
-                stk[sp * stride] = (unsigned short)((cur << 4) | msk);
-                ++sp;
-            }
+            if (msk) StackPush(stk, stride, sp, cur, msk, st);
             cur = lrt::libm::f2u_i(bv.nodes[8 * cur + 2 * c].w);
             msk = 0xF;
-#endif
         }
     }
     tOut = bestT;
-    return (LRT_BVH_LAZY_ID && best >= 0) ? bv.lid[best] : best;
+    return best >= 0 ? bv.lid[best] : best;
 }
 
 LRT_DEV int ClosestHitBVH4(const F3& o, const F3& d, const BvhView& bv, float& tOut, unsigned short* stk, int stride,
                            BvhStats* st = nullptr) {
     const SlabRay sr = MakeSlabRay(o, d, bv.margin);
-    if (!LRT_BVH_SLAB_SPLIT) return ClosestHitBVH4Impl<0>(o, d, sr, bv, tOut, stk, stride, st);
     if (sr.fma) return ClosestHitBVH4Impl<1>(o, d, sr, bv, tOut, stk, stride, st);
     return ClosestHitBVH4Impl<2>(o, d, sr, bv, tOut, stk, stride, st);
 }
 
+// Light sampling's `HitWorld(shadow ray) && hitID == li` (parallel.cpp:122-123) through
+// the BVH. (cand_li, li) must be the lexicographic minimum, so the light's own candidate
+// is the bar from the start: boxes beyond it are culled (same conservative margins) and
+// the first sphere that beats it -- cand_j < cand_li, or equal with j < li -- ends the
+// traversal. Same per-sphere arithmetic as the scan, so the answer is bit-identical.
+LRT_DEV float SphereCand(const F3& o, const F3& d, const float4& s) {   // maths.cpp:54-90
+    const F3 rs = f3(s.x, s.y, s.z) - o;
+    const float rsProj = dot(rs, d);
+    const float ifHit = dot(rs, rs) - rsProj * rsProj - s.w;
+    if (!(ifHit < 0.0f)) return __builtin_inff();
+    const float halfCut = sqrt_rn(-ifHit);
+    const float t1 = rsProj - halfCut;
+    const float t2 = rsProj + halfCut;
+    return t1 > kMinT ? t1 : (t2 > kMinT ? t2 : __builtin_inff());
+}
 template <int kForm>
 LRT_DEV bool ShadowReachesLightBVH4Impl(const F3& o, const F3& d, int li, float candL, const SlabRay& sr,
-                                        const BvhView& bv, unsigned short* stk, int stride) {
+                                        const BvhView& bv, unsigned short* stk, int stride, BvhStats* st) {
     // (cand, index) beats the light's (candL, li); the index is read only on an exact tie
     auto beats = [&](float c, int pos) { return c < candL || (c == candL && bv.lid[pos] < li); };
-    bool blocked = false;
-    auto test = [&](int pos, const float4& s) { blocked = blocked || beats(SphereCand(o, d, s), pos); };
     for (int j = 0; j < bv.nbig; ++j)
         if (beats(SphereCand(o, d, bv.lsph[bv.big0 + j]), bv.big0 + j)) return false;
     if (bv.nnodes == 0) return true;
@@ -422,16 +237,11 @@ LRT_DEV bool ShadowReachesLightBVH4Impl(const F3& o, const F3& d, int li, float 
     for (;;) {
         int next = -1, rem = 0, nextRef = 0;
         float nearT = __builtin_inff();
-        float4 nd[8];
-        if (LRT_BVH_PRELOAD) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) nd[k] = bv.nodes[8 * cur + k];
-        }
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             if (!((msk >> c) & 1)) continue;
-            const float4 lo = LRT_BVH_PRELOAD ? nd[2 * c] : bv.nodes[8 * cur + 2 * c];
-            const float4 hi = LRT_BVH_PRELOAD ? nd[2 * c + 1] : bv.nodes[8 * cur + 2 * c + 1];
+            const float4 lo = bv.nodes[8 * cur + 2 * c];
+            const float4 hi = bv.nodes[8 * cur + 2 * c + 1];
             const int cnt = lrt::libm::f2u_i(hi.w);
             if (cnt < 0) continue;
             float tn, tf;
@@ -440,8 +250,9 @@ LRT_DEV bool ShadowReachesLightBVH4Impl(const F3& o, const F3& d, int li, float 
             const float tfm = tf + m;   // (tn <= tf + m, tn <= candL + mb, tf + m >= kMinT)
             if (!(tn <= __builtin_fminf(tfm, candL + mb) && tfm >= kMinT)) continue;
             if (cnt > 0) {
-                ForLeafSpheres(bv.lsph, lrt::libm::f2u_i(lo.w), cnt, test);
-                if (blocked) return false;
+                const int ref = lrt::libm::f2u_i(lo.w);
+                for (int j = 0; j < cnt; ++j)
+                    if (beats(SphereCand(o, d, bv.lsph[ref + j]), ref + j)) return false;
             } else {
                 rem |= 1 << c;
                 if (tn < nearT) {
@@ -453,10 +264,7 @@ LRT_DEV bool ShadowReachesLightBVH4Impl(const F3& o, const F3& d, int li, float 
         }
         if (next >= 0) {
             rem &= ~(1 << next);
-            if (rem) {
-                stk[sp * stride] = (unsigned short)((cur << 4) | rem);
-                ++sp;
-            }
+            if (rem) StackPush(stk, stride, sp, cur, rem, st);
             cur = nextRef;
             msk = 0xF;
         } else {
@@ -469,10 +277,7 @@ LRT_DEV bool ShadowReachesLightBVH4Impl(const F3& o, const F3& d, int li, float 
             // into the first without testing again, push the rest back
             const int c = __builtin_ctz(msk);
             msk &= msk - 1;
-            if (msk) {
-                stk[sp * stride] = (unsigned short)((cur << 4) | msk);
-                ++sp;
-            }
+            if (msk) StackPush(stk, stride, sp, cur, msk, st);
             cur = lrt::libm::f2u_i(bv.nodes[8 * cur + 2 * c].w);
             msk = 0xF;
         }
@@ -481,14 +286,14 @@ LRT_DEV bool ShadowReachesLightBVH4Impl(const F3& o, const F3& d, int li, float 
 }
 
 LRT_DEV bool ShadowReachesLightBVH4(const F3& o, const F3& d, int li, const float4& lightSph, const BvhView& bv,
-                                    unsigned short* stk, int stride) {
+                                    unsigned short* stk, int stride, BvhStats* st = nullptr) {
     const float candL = SphereCand(o, d, lightSph);
     if (!(candL < kMaxT)) return false;   // the light is not hit at all (closestT starts at kMaxT)
     const SlabRay sr = MakeSlabRay(o, d, bv.margin);
-    if (!LRT_BVH_SLAB_SPLIT) return ShadowReachesLightBVH4Impl<0>(o, d, li, candL, sr, bv, stk, stride);
-    if (sr.fma) return ShadowReachesLightBVH4Impl<1>(o, d, li, candL, sr, bv, stk, stride);
-    return ShadowReachesLightBVH4Impl<2>(o, d, li, candL, sr, bv, stk, stride);
+    if (sr.fma) return ShadowReachesLightBVH4Impl<1>(o, d, li, candL, sr, bv, stk, stride, st);
+    return ShadowReachesLightBVH4Impl<2>(o, d, li, candL, sr, bv, stk, stride, st);
 }
+
 
 // Two queries from one origin in ONE traversal loop (the pool kernel's bounce step,
 // lrt_pool.h): first the deferred shadow ray of the last scatter's last light (ds, light
@@ -583,7 +388,7 @@ LRT_DEV void TravInit(TravQuery& q, const F3& o, const F3& db, bool hasS, const 
 
 // One node visit of the lane's current query; at a query's end the shadow query hands over
 // to the bounce query, and the bounce query clears `busy`.
-LRT_DEV void TravStep(TravQuery& q, const BvhView& bv, unsigned short* stk, int stride) {
+LRT_DEV void TravStep(TravQuery& q, const BvhView& bv, unsigned short* stk, int stride, BvhStats* st = nullptr) {
     bool qdone = q.msk == 0 || (q.sh && q.best != -2);   // stack exhausted, or the light is beaten
     if (!qdone) {
         const float mb = bv.margin + q.sr.mo + 1e-5f * q.bestT;
@@ -636,10 +441,7 @@ LRT_DEV void TravStep(TravQuery& q, const BvhView& bv, unsigned short* stk, int 
         }
         if (next >= 0) {
             rem &= ~(1 << next);
-            if (rem) {
-                stk[q.sp * stride] = (unsigned short)((q.cur << 4) | rem);
-                ++q.sp;
-            }
+            if (rem) StackPush(stk, stride, q.sp, q.cur, rem, st);
             q.cur = nextRef;
             q.msk = 0xF;
         } else if (q.sp == 0) {
@@ -650,10 +452,7 @@ LRT_DEV void TravStep(TravQuery& q, const BvhView& bv, unsigned short* stk, int 
             int cur = e >> 4, msk = e & 0xF;
             const int c = __builtin_ctz(msk);
             msk &= msk - 1;
-            if (msk) {
-                stk[q.sp * stride] = (unsigned short)((cur << 4) | msk);
-                ++q.sp;
-            }
+            if (msk) StackPush(stk, stride, q.sp, cur, msk, st);
             q.cur = lrt::libm::f2u_i(bv.nodes[8 * cur + 2 * c].w);
             q.msk = 0xF;
         }
@@ -675,10 +474,11 @@ LRT_DEV int TravResult(const TravQuery& q, const BvhView& bv, float& tOut) {
 }
 
 LRT_DEV int ClosestHitDualBVH4(const F3& o, const F3& db, bool hasS, const F3& ds, int li, const float4& lightSph,
-                               const BvhView& bv, float& tOut, bool& lit, unsigned short* stk, int stride) {
+                               const BvhView& bv, float& tOut, bool& lit, unsigned short* stk, int stride,
+                               BvhStats* st = nullptr) {
     TravQuery q;
     TravInit(q, o, db, hasS, ds, li, lightSph, bv);
-    while (q.busy) TravStep(q, bv, stk, stride);
+    while (q.busy) TravStep(q, bv, stk, stride, st);
     lit = q.lit;
     return TravResult(q, bv, tOut);
 }
@@ -843,23 +643,23 @@ __device__ __forceinline__ bool ShadowPacket(const F3& o, const F3& d, int li, f
 #define LRT_PACKET_AVAILABLE 0
 #endif
 
-// The layout the host built (build_bvh_host): 4-wide unless LRT_BVH4=0. coherent: the
+// The 4-wide layout the host built (build_bvh_host). coherent: the
 // caller's active lanes are rays that start together (packet traversal when every one of
 // them takes the FMA slab form).
 LRT_DEV int ClosestHitBVH(const F3& o, const F3& d, const BvhView& bv, float& tOut, unsigned short* stk, int stride,
                           BvhStats* st = nullptr, bool coherent = false) {
-#if LRT_PACKET_AVAILABLE && LRT_BVH4
+#if LRT_PACKET_AVAILABLE
     if (coherent) {
         const SlabRay sr = MakeSlabRay(o, d, bv.margin);
         if (__ballot(!sr.fma) == 0) return ClosestHitPacket(o, d, sr, bv, tOut, stk, stride);
     }
 #endif
     (void)coherent;
-    return LRT_BVH4 ? ClosestHitBVH4(o, d, bv, tOut, stk, stride, st) : ClosestHitBVH2(o, d, bv, tOut, stk, stride, st);
+    return ClosestHitBVH4(o, d, bv, tOut, stk, stride, st);
 }
 LRT_DEV bool ShadowReachesLightBVH(const F3& o, const F3& d, int li, const float4& lightSph, const BvhView& bv,
-                                   unsigned short* stk, int stride, bool coherent = false) {
-#if LRT_PACKET_AVAILABLE && LRT_BVH4
+                                   unsigned short* stk, int stride, bool coherent = false, BvhStats* st = nullptr) {
+#if LRT_PACKET_AVAILABLE
     if (coherent) {
         const float candL = SphereCand(o, d, lightSph);
         const SlabRay sr = MakeSlabRay(o, d, bv.margin);
@@ -867,8 +667,7 @@ LRT_DEV bool ShadowReachesLightBVH(const F3& o, const F3& d, int li, const float
     }
 #endif
     (void)coherent;
-    return LRT_BVH4 ? ShadowReachesLightBVH4(o, d, li, lightSph, bv, stk, stride)
-                    : ShadowReachesLightBVH2(o, d, li, lightSph, bv, stk, stride);
+    return ShadowReachesLightBVH4(o, d, li, lightSph, bv, stk, stride, st);
 }
 
 }  // namespace lrt

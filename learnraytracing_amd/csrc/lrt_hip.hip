@@ -206,7 +206,6 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
     sc.pow.exp2 = reinterpret_cast<const uint64_t*>(s_pow + 32);
     sc.rnlut = s_lut;
     sc.sph = kLds ? s_sph : a.sph;
-    sc.gsph = a.sph;
     sc.mats = kLds ? s_mat : a.mats;
     sc.lights = kLds ? s_lights : a.lights;
     sc.count = a.count;
@@ -816,8 +815,7 @@ void build_bvh_host(const lrt_sphere* s, int n, const std::vector<float4>& sph, 
         B.lid.push_back(i);
     }
     out.nbig = (int)big.size();
-    out.stack_levels = B.max_depth + 1;
-#if LRT_BVH4
+    out.stack_levels = 1;
     if (!B.nodes.empty()) {   // collapse the BVH2 into 4-wide nodes (grandchildren of each node)
         auto ival = [](float f) { int v; memcpy(&v, &f, 4); return v; };
         auto fval = [](int v) { float f; memcpy(&f, &v, 4); return f; };
@@ -859,9 +857,10 @@ void build_bvh_host(const lrt_sphere* s, int n, const std::vector<float4>& sph, 
         };
         collapse(0, 0);
         B.nodes.swap(n4);
-        out.stack_levels = depth4 + 1;   // one (node, child mask) entry per level
+        // a traversal holds at most one (node, child mask) entry per level above its node
+        // (StackPush, lrt_bvh.h): depth4 entries; one spare
+        out.stack_levels = depth4 + 1;
     }
-#endif
     out.nodes.swap(B.nodes);
     out.lsph.swap(B.lsph);
     out.lid.swap(B.lid);
@@ -926,6 +925,9 @@ int upload_scene(Context& c, const lrt_sphere* s, const lrt_material* m, int n) 
     if (n > kBvhMinSpheres) {
         BvhHost B;
         build_bvh_host(s, n, sph, B);
+        // the LDS traversal stack is sized to B.stack_levels entries per lane, which bounds
+        // every push (StackPush: at most one entry per level above the current node)
+        if (B.stack_levels > kBvhStackLevels) return fail(LRT_E_INVALID, "BVH deeper than the traversal stack");
         LRT_HIP(hipMalloc(&c.d_bvh_nodes, sizeof(float4) * std::max<size_t>(B.nodes.size(), 4)));
         LRT_HIP(hipMalloc(&c.d_bvh_lsph, sizeof(float4) * B.lsph.size()));
         LRT_HIP(hipMalloc(&c.d_bvh_lid, sizeof(int) * B.lid.size()));
@@ -933,7 +935,7 @@ int upload_scene(Context& c, const lrt_sphere* s, const lrt_material* m, int n) 
             LRT_HIP(hipMemcpy(c.d_bvh_nodes, B.nodes.data(), sizeof(float4) * B.nodes.size(), hipMemcpyHostToDevice));
         LRT_HIP(hipMemcpy(c.d_bvh_lsph, B.lsph.data(), sizeof(float4) * B.lsph.size(), hipMemcpyHostToDevice));
         LRT_HIP(hipMemcpy(c.d_bvh_lid, B.lid.data(), sizeof(int) * B.lid.size(), hipMemcpyHostToDevice));
-        c.bvh_nodes = (int)(B.nodes.size() / (LRT_BVH4 ? 8 : 4));
+        c.bvh_nodes = (int)(B.nodes.size() / 8);
         c.bvh_big0 = B.big0;
         c.bvh_nbig = B.nbig;
         c.bvh_margin = B.margin;
@@ -1438,17 +1440,28 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
 }
 
 // Pixels per pool tile: a round holds kPoolSamples samples, so more frames -> fewer pixels.
-template <int MAXD>
-int launch_pool_split(const KernelArgs& a, bool lds, int xc, int rows, int frames, hipStream_t s) {
+// Bigger tiles make bigger pools (a round's tail, its last paths with most lanes idle, is a
+// smaller share) but fewer tiles per wave (the launch's tail).
+int pool_pixels(int frames) {
     static const int cap = [] {   // LRT_POOL_PIX_MAX: largest tile (A/B)
         const char* e = getenv("LRT_POOL_PIX_MAX");
         return e ? atoi(e) : 64;
     }();
-    if (cap >= 64 && 64 * frames <= kPoolSamples) return launch_pool<MAXD, 64>(a, lds, xc, rows, s);
-    if (cap >= 32 && 32 * frames <= kPoolSamples) return launch_pool<MAXD, 32>(a, lds, xc, rows, s);
-    if (cap >= 16 && 16 * frames <= kPoolSamples) return launch_pool<MAXD, 16>(a, lds, xc, rows, s);
-    if (4 * frames <= kPoolSamples) return launch_pool<MAXD, 4>(a, lds, xc, rows, s);
-    return launch_pool<MAXD, 1>(a, lds, xc, rows, s);
+    for (int pix : {256, 128, 64, 32, 16})
+        if (cap >= pix && pix * frames <= kPoolSamples) return pix;
+    return 4 * frames <= kPoolSamples ? 4 : 1;
+}
+template <int MAXD>
+int launch_pool_split(const KernelArgs& a, bool lds, int xc, int rows, int frames, hipStream_t s) {
+    switch (pool_pixels(frames)) {
+        case 256: return launch_pool<MAXD, 256>(a, lds, xc, rows, s);
+        case 128: return launch_pool<MAXD, 128>(a, lds, xc, rows, s);
+        case 64: return launch_pool<MAXD, 64>(a, lds, xc, rows, s);
+        case 32: return launch_pool<MAXD, 32>(a, lds, xc, rows, s);
+        case 16: return launch_pool<MAXD, 16>(a, lds, xc, rows, s);
+        case 4: return launch_pool<MAXD, 4>(a, lds, xc, rows, s);
+        default: return launch_pool<MAXD, 1>(a, lds, xc, rows, s);
+    }
 }
 
 // v4 (lrt_wavefront.h): chunks of whole pixels, maxDepth + 1 extend/shade rounds each,
@@ -1655,9 +1668,8 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
 int auto_kernel(const KernelArgs& a, const lrt_render_desc* d, bool feat) {
     if (feat || d->frames < 4) return LRT_F_SIMPLE;
     if (!(a.bv.on || d->max_depth > 8) && !pool_order_on()) return LRT_F_SIMPLE;
-    int pix = 64;
-    while (pix > 1 && pix * d->frames > kPoolSamples) pix /= (pix == 64 || pix == 32 ? 2 : 4);
-    const int tx = pix >= 32 ? 8 : pix >= 8 ? 4 : pix >= 2 ? 2 : 1, ty = pix / tx;
+    const int pix = pool_pixels(d->frames);
+    const int tx = pix >= 128 ? 16 : pix >= 32 ? 8 : pix >= 8 ? 4 : pix >= 2 ? 2 : 1, ty = pix / tx;
     const long long tiles = (long long)((d->x_count + tx - 1) / tx) * ((d->row_count + ty - 1) / ty);
     const long long slots = 16LL * ctx().num_cus;   // resident waves (4 per SIMD)
     return tiles >= 2 * slots ? LRT_F_POOL : LRT_F_SIMPLE;
@@ -1723,6 +1735,12 @@ int host_unregister(void* p) {
             return LRT_OK;
         }
     return fail(LRT_E_INVALID, "not a buffer the library registered");
+}
+
+bool host_registered_here(const void* p) {
+    for (const auto& r : g_host_regs)
+        if (r.p == p) return true;
+    return false;
 }
 
 // The device address of pageable buf once it is registered (see above), else nullptr.
@@ -1997,8 +2015,8 @@ int render_host(const lrt_render_desc* d, float* buf, long long* out_rays, const
         snprintf(g_last_launch + n, sizeof(g_last_launch) - n, " host=%s%s", registered ? "registered-" : "", path);
     };
     float* hdev = (!feat && host_zero_copy()) ? host_pinned(buf) : nullptr;
-    const bool registered =
-        allow_register && !hdev && !feat && host_zero_copy() && (hdev = host_register(buf, bytes)) != nullptr;
+    bool registered = hdev && host_registered_here(buf);
+    if (allow_register && !hdev && !feat && host_zero_copy()) registered = (hdev = host_register(buf, bytes)) != nullptr;
     if (hdev && host_pipeline(d, bytes)) {
         if ((rc = ensure_frame(bytes))) return rc;
         if ((rc = render_host_pipelined(d, buf, hdev, bytes, out_rays))) return rc;
@@ -2551,10 +2569,10 @@ int lrt_bvh_stats(const lrt_sphere* spheres, int count, const float* rays, int n
     bv.lid = H.lid.data();
     bv.margin = H.margin;
     bv.on = 1;
-    bv.nnodes = (int)(H.nodes.size() / (LRT_BVH4 ? 8 : 4));
+    bv.nnodes = (int)(H.nodes.size() / 8);
     bv.big0 = H.big0;
     bv.nbig = H.nbig;
-    double sn = 0, ss = 0, mn = 0, ms = 0, bad = 0;
+    double sn = 0, ss = 0, mn = 0, ms = 0, bad = 0, msp = 0;
     unsigned short stk[kBvhStackLevels];
     for (int i = 0; i < n; ++i) {
         const Ray r = make_ray(f3(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]),
@@ -2566,12 +2584,12 @@ int lrt_bvh_stats(const lrt_sphere* spheres, int count, const float* rays, int n
         if (a != b || memcmp(&t1, &t2, 4) != 0) bad += 1;
         // the bounded shadow-ray traversal: true for the scan's winner, and for any other
         // sphere exactly when it is the winner
-        if (b >= 0 && !ShadowReachesLightBVH(r.orig, r.dir, b, sph[b], bv, stk, 1)) bad += 1;
+        if (b >= 0 && !ShadowReachesLightBVH(r.orig, r.dir, b, sph[b], bv, stk, 1, false, &st)) bad += 1;
         const int other = (int)(((unsigned)i * 7919u) % (unsigned)count);
-        if (ShadowReachesLightBVH(r.orig, r.dir, other, sph[other], bv, stk, 1) != (b == other)) bad += 1;
+        if (ShadowReachesLightBVH(r.orig, r.dir, other, sph[other], bv, stk, 1, false, &st) != (b == other)) bad += 1;
         // the two-query loop (pool kernel): this ray as the shadow ray towards `other` (and
         // towards the winner), the next ray's direction from the same origin as the bounce ray
-        if (LRT_BVH4) {
+        {
             const int i2 = (i + 1) % n;
             const Ray r2 = make_ray(r.orig, f3(rays[6 * i2 + 3], rays[6 * i2 + 4], rays[6 * i2 + 5]));
             float t3, t4;
@@ -2579,16 +2597,17 @@ int lrt_bvh_stats(const lrt_sphere* spheres, int count, const float* rays, int n
             for (int li : {other, b}) {
                 if (li < 0) continue;
                 bool lit = true;
-                const int c3 = ClosestHitDualBVH4(r.orig, r2.dir, true, r.dir, li, sph[li], bv, t4, lit, stk, 1);
+                const int c3 = ClosestHitDualBVH4(r.orig, r2.dir, true, r.dir, li, sph[li], bv, t4, lit, stk, 1, &st);
                 if (c3 != c2 || memcmp(&t3, &t4, 4) != 0 || lit != (b == li)) bad += 1;
             }
             bool lit = true;
-            const int c4 = ClosestHitDualBVH4(r.orig, r2.dir, false, r.dir, 0, sph[0], bv, t4, lit, stk, 1);
+            const int c4 = ClosestHitDualBVH4(r.orig, r2.dir, false, r.dir, 0, sph[0], bv, t4, lit, stk, 1, &st);
             if (c4 != c2 || memcmp(&t3, &t4, 4) != 0 || lit) bad += 1;
         }
         sn += st.nodes;
         ss += st.spheres;
         mn = std::max(mn, (double)st.nodes);
+        msp = std::max(msp, (double)st.max_sp);
         ms = std::max(ms, (double)st.spheres);
     }
     out[0] = sn / n;
@@ -2596,6 +2615,8 @@ int lrt_bvh_stats(const lrt_sphere* spheres, int count, const float* rays, int n
     out[2] = mn;
     out[3] = ms;
     out[4] = bad / n;
+    out[5] = msp;                    // deepest stack entry any traversal wrote
+    out[6] = (double)H.stack_levels; // the entries the LDS stack holds for this scene
     return LRT_OK;
 }
 
@@ -2621,11 +2642,11 @@ int lrt_scatter_eval(const lrt_sphere* spheres, const lrt_material* materials, i
     sc.rnlut = nullptr;
     sc.bv.margin = B.margin;
     sc.bv.on = bvh ? 1 : 0;
-    sc.bv.nnodes = bvh ? (int)(B.nodes.size() / (LRT_BVH4 ? 8 : 4)) : 0;
+    sc.bv.nnodes = bvh ? (int)(B.nodes.size() / 8) : 0;
     sc.bv.big0 = B.big0;
     sc.bv.nbig = B.nbig;
     if (!on_device) {
-        sc.sph = sc.gsph = sph.data();
+        sc.sph = sph.data();
         sc.mats = mats.data();
         sc.lights = lights.data();
         sc.bv.nodes = B.nodes.data();
@@ -2670,7 +2691,7 @@ int lrt_scatter_eval(const lrt_sphere* spheres, const lrt_material* materials, i
         release();
         return fail(LRT_E_NOMEM, "scatter probe: device allocation failed");
     }
-    sc.sph = sc.gsph = (const float4*)dd[0];
+    sc.sph = (const float4*)dd[0];
     sc.mats = (const float4*)dd[1];
     sc.lights = (const int*)dd[2];
     sc.bv.nodes = (const float4*)dd[3];
@@ -2708,7 +2729,7 @@ int lrt_bvh_eval(const lrt_sphere* spheres, int count, const float* rays, int n,
     BvhView bv;
     bv.margin = H.margin;
     bv.on = 1;
-    bv.nnodes = (int)(H.nodes.size() / (LRT_BVH4 ? 8 : 4));
+    bv.nnodes = (int)(H.nodes.size() / 8);
     bv.big0 = H.big0;
     bv.nbig = H.nbig;
     if (mode == 0) {

@@ -38,9 +38,9 @@ enum : int { kPoolIdle = 0, kPoolTrace = 1, kPoolDone = 2, kPoolEnded = 3 };
 
 template <int kPix>
 struct PoolTile {   // tile shape: kPix pixels, as square as a power of two allows
-    static constexpr int X = kPix >= 32 ? 8 : kPix >= 8 ? 4 : kPix >= 2 ? 2 : 1;
+    static constexpr int X = kPix >= 128 ? 16 : kPix >= 32 ? 8 : kPix >= 8 ? 4 : kPix >= 2 ? 2 : 1;
     static constexpr int Y = kPix / X;
-    static_assert(X * Y == kPix && kPix <= 64, "kPix: a power of two up to 64");
+    static_assert(X * Y == kPix && kPix <= 256, "kPix: a power of two up to 256");
 };
 
 template <int MAXD, bool kLds, bool kBvh, int kPix, int kNS = 0>
@@ -77,7 +77,6 @@ __global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const Ker
     sc.pow.exp2 = reinterpret_cast<const uint64_t*>(s_pow + 32);
     sc.rnlut = s_lut;
     sc.sph = kLds ? s_sph : a.sph;
-    sc.gsph = a.sph;
     sc.mats = kLds ? s_mat : a.mats;
     sc.lights = kLds ? s_lights : a.lights;
     sc.count = a.count;
@@ -278,28 +277,31 @@ __global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const Ker
                 }
             }
             // ---- the round's colours in frame order, one lane per pixel (:262,282) ---------
-            // Lane j < kPix owns pixel j of the tile. Its address and previous value are
+            // Lane j owns pixels j, j + 64, ... of the tile. Its address and previous value are
             // taken here, not held in registers through the bounce loop (fewer live VGPRs in
             // the traversal); a later round re-reads what this one wrote.
             sec_enter(sc, kSecOther, false);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            const int mx = tx0 + lane % TX, my = ty0 + (lane / TX) % TY;
-            const bool mine = lane < kPix && mx < a.xc && my < a.rows;
-            if (mine) {
-                float4* const mpx = a.out + (size_t)my * a.xc + mx;
-                float4 acc = *mpx;
-                F3 c3 = f3(acc.x, acc.y, acc.z);
-                for (int t = 0; t < nfr; ++t) {
-                    const float4 c = slots[t * kPix + lane];
-                    const int f = fr0 + t;
-                    const float lerpFac = f < kLerpTable ? a.lerp[f] : (float)f / (float)(f + 1);
-                    c3 = c3 * lerpFac + f3(c.x, c.y, c.z) * (1.0f - lerpFac);
+#pragma unroll
+            for (int j0 = 0; j0 < kPix; j0 += 64) {   // tiles above 64 pixels: several per lane
+                const int j = j0 + lane;
+                const int mx = tx0 + j % TX, my = ty0 + (j / TX) % TY;
+                if (j < kPix && mx < a.xc && my < a.rows) {
+                    float4* const mpx = a.out + (size_t)my * a.xc + mx;
+                    float4 acc = *mpx;
+                    F3 c3 = f3(acc.x, acc.y, acc.z);
+                    for (int t = 0; t < nfr; ++t) {
+                        const float4 c = slots[t * kPix + j];
+                        const int f = fr0 + t;
+                        const float lerpFac = f < kLerpTable ? a.lerp[f] : (float)f / (float)(f + 1);
+                        c3 = c3 * lerpFac + f3(c.x, c.y, c.z) * (1.0f - lerpFac);
+                    }
+                    acc.x = c3.x;
+                    acc.y = c3.y;
+                    acc.z = c3.z;
+                    *mpx = acc;   // alpha as read
                 }
-                acc.x = c3.x;
-                acc.y = c3.y;
-                acc.z = c3.z;
-                *mpx = acc;   // alpha as read
             }
             // the next round overwrites the slots: every read above completes first
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");

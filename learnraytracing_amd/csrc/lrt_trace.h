@@ -213,17 +213,8 @@ LRT_DEV Material load_material(const float4* __restrict__ mats, int id) {
 #include "lrt_bvh.h"
 namespace lrt {
 
-// LRT_SCALAR_SCENE=1: the linear closest-hit scan (uniform sphere index) reads spheres
-// through the constant address space, i.e. scalar loads into SGPRs, instead of LDS.
-// Measured slower than the LDS broadcast reads (config 2: 0.409 vs 0.394 ms), so off.
-#ifndef LRT_SCALAR_SCENE
-#define LRT_SCALAR_SCENE 0
-#endif
-typedef const __attribute__((address_space(4))) float* ConstFPtr;
-
 struct SceneView {
     const float4* sph;                 // LDS or global
-    const float4* gsph;                // the same spheres in global memory (scalar loads)
     const float4* __restrict__ mats;   // global (per-lane gather, L1/L2 resident)
     const int* __restrict__ lights;    // emissive sphere ids in index order
     int count;
@@ -272,23 +263,10 @@ LRT_DEV void sec_enter(const SceneView& sc, int sec, bool count) {
 LRT_DEV void sec_count(const SceneView& sc, int sec) { sec_enter(sc, sec, true); }
 
 // HitSphere's root selection against the running closestT (maths.cpp:61-90): the first
-// root if it lies in (tMin, closestT), else the second. LRT_BRANCHLESS_HIT evaluates it
-// with selects for every lane (sqrt of a dummy 1 where the ray misses) instead of a
-// divergent branch around the sqrt; same values either way.
-#ifndef LRT_BRANCHLESS_HIT
-#define LRT_BRANCHLESS_HIT 0
-#endif
+// root if it lies in (tMin, closestT), else the second. (A branchless form -- sqrt for every
+// lane, selects -- measured slower: the divergent branch around the sqrt is cheap when no
+// lane takes it.)
 LRT_DEV void SphereRoots(float rsProj, float ifHit, float tMin, float& closestT, int& id, int i) {
-#if LRT_BRANCHLESS_HIT
-    const bool h = ifHit < 0.0f;
-    const float halfCut = sqrt_rn(h ? -ifHit : 1.0f);
-    const float t1 = rsProj - halfCut;
-    const float t2 = rsProj + halfCut;
-    const bool c1 = h && t1 > tMin && t1 < closestT;
-    const bool c2 = h && !c1 && t2 > tMin && t2 < closestT;
-    closestT = c1 ? t1 : (c2 ? t2 : closestT);
-    id = (c1 || c2) ? i : id;
-#else
     if (ifHit < 0.0f) {
         const float halfCut = sqrt_rn(-ifHit);
         float t = rsProj - halfCut;
@@ -303,7 +281,6 @@ LRT_DEV void SphereRoots(float rsProj, float ifHit, float tMin, float& closestT,
             }
         }
     }
-#endif
 }
 
 // HitWorld + HitSphere (parallel.cpp:54-73, maths.cpp:51-94). The per-sphere test
@@ -319,8 +296,6 @@ LRT_DEV int ClosestHitSV(const Ray& r, float tMin, float tMax, const SceneView& 
         return ClosestHitBVH(r.orig, r.dir, sc.bv, tOut, sc.bstk, sc.bstride, nullptr, coherent);
     float closestT = tMax;
     int id = -1;
-    const ConstFPtr csph = (ConstFPtr)sc.gsph;
-    auto cload = [&](int i) { return make_float4(csph[4 * i], csph[4 * i + 1], csph[4 * i + 2], csph[4 * i + 3]); };
     auto test = [&](int i, const float4& s) {
         F3 rs = f3(s.x, s.y, s.z) - r.orig;
         float rsProj = dot(rs, r.dir);
@@ -331,10 +306,10 @@ LRT_DEV int ClosestHitSV(const Ray& r, float tMin, float tMax, const SceneView& 
 #pragma unroll
         for (int i = 0; i < kNS; ++i) test(i, sc.sph[i]);
     } else {
-        float4 next = LRT_SCALAR_SCENE ? cload(0) : sc.sph[0];   // one sphere ahead (SGPRs or VGPRs)
+        float4 next = sc.sph[0];   // one sphere ahead
         for (int i = 0; i < sc.count; ++i) {
             const float4 s = next;
-            if (i + 1 < sc.count) next = LRT_SCALAR_SCENE ? cload(i + 1) : sc.sph[i + 1];
+            if (i + 1 < sc.count) next = sc.sph[i + 1];
             test(i, s);
         }
     }

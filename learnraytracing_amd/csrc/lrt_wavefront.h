@@ -84,7 +84,6 @@ __device__ __forceinline__ SceneView wf_scene(const KernelArgs& a, bool lds, int
     sc.pow.exp2 = reinterpret_cast<const uint64_t*>(s_pow + 32);
     sc.rnlut = s_lut;
     sc.sph = lds ? s_sph : a.sph;
-    sc.gsph = a.sph;
     sc.mats = lds ? s_mat : a.mats;
     sc.lights = lds ? s_lights : a.lights;
     sc.count = a.count;

@@ -13,8 +13,11 @@ from learnraytracing_amd.scene import random_scene
 def stats(spheres, rays):
     sa = (L.Sphere * len(spheres))(*spheres)
     rays = np.ascontiguousarray(rays, np.float32)
-    out = (ctypes.c_double * 5)()
+    out = (ctypes.c_double * 7)()
     L.check(L.lib().lrt_bvh_stats(sa, len(spheres), rays.ctypes.data_as(ctypes.c_void_p), len(rays), out))
+    # the LDS stack guard: no traversal (closest hit, shadow, two-query) writes an entry beyond
+    # the levels the device stack is sized to for this scene
+    assert 0 <= out[5] <= out[6] <= 24, list(out)
     return list(out)
 
 
@@ -74,6 +77,28 @@ def test_axis_aligned_and_surface_rays():
         nrm /= np.linalg.norm(nrm)
         rays.append(np.concatenate([c + s.radius * nrm, g.normal(size=3)]))
     assert stats(sph, np.array(rays, np.float32))[4] == 0.0
+
+
+@pytest.mark.parametrize("n,leaf", [(4096, 1), (4096, 16), (1000, 2)])
+def test_stack_depth_bound_deepest_trees(monkeypatch, n, leaf):
+    """The deepest trees the builder makes (leaf size 1: 4096 leaves; a colinear chain of
+    spheres whose median splits recurse to the depth cap): every traversal's stack stays
+    within the LDS allocation (parallel.cpp:54-73's HitWorld answer unchanged)."""
+    monkeypatch.setenv("LRT_BVH_LEAF", str(leaf))
+    g = np.random.default_rng(n + leaf)
+    sph, _ = random_scene(n, 1)
+    res = stats(sph, random_rays(g, 3000, [-6, -0.6, -7], [6, 3, 4]))
+    assert res[4] == 0.0 and res[5] >= 1
+    chain = [L.Sphere(L.f3(0.01 * i, 0.0, 0.0), 0.004) for i in range(n)]   # colinear, tiny
+    o = np.zeros((3000, 3))
+    o[:, 0] = g.uniform(-1, 0.01 * n + 1, 3000)
+    o[:, 1] = g.uniform(-0.01, 0.01, 3000)
+    o[:, 2] = -1.0
+    d = np.tile([0.0, 0.0, 1.0], (3000, 1)) + g.normal(0, 0.002, (3000, 3))
+    rays = np.concatenate([o, d], axis=1).astype(np.float32)
+    rays2 = np.concatenate([np.array([[-1.0, 0.0, 0.0]] * 100), np.tile([1.0, 0.0, 0.0], (100, 1))], axis=1)
+    res = stats(chain, np.concatenate([rays, rays2.astype(np.float32)]))
+    assert res[4] == 0.0
 
 
 @pytest.mark.parametrize("bad", [1, 40])

@@ -29,8 +29,8 @@ for i in range(m):
         out[:3] = cam[:3]
         out[3:] = cam[12:15] + u * cam[15:18] + v * cam[18:21] - cam[:3]
     rays[i] = out
-res = (ctypes.c_double * 5)()
+res = (ctypes.c_double * 7)()
 sa = (L.Sphere * n)(*sph)
 L.check(L.lib().lrt_bvh_stats(sa, n, rays.ctypes.data_as(ctypes.c_void_p), m, res))
 print(f"n={n}: nodes/ray {res[0]:.1f} spheres/ray {res[1]:.1f} max nodes {res[2]:.0f} "
-      f"max spheres {res[3]:.0f} mismatch {res[4]:.4f}")
+      f"max spheres {res[3]:.0f} mismatch {res[4]:.4f} stack {res[5]:.0f} of {res[6]:.0f} levels")
