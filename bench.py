@@ -6,9 +6,11 @@
 
 A step is one pass of the hot path over one batch: every rank renders its
 row-block-cyclic share of the config's W x H image at the config's spp (one kernel
-launch), and for N > 1 the shards are gathered to rank 0 over RCCL and assembled there
-(the gather of step k overlaps the render of step k+1; the timed region ends after the
-last gather and assembly).
+launch). For N > 1 the frame is assembled on rank 0 by the renders themselves: each
+rank's render stores its finished pixels into rank 0's frame over xGMI (IPC-mapped;
+--exchange rccl instead packs to RGB, gathers over RCCL and assembles with the unshard
+kernel, the gather of step k overlapping the render of step k+1); the timed region ends when
+every rank's last render (and gather/assembly) has completed.
 
 Scaling is STRONG by default: the frame (W x H x spp) is fixed and split over the N
 GPUs, so config 2 at N = 8 is still 1280x720 at 4 spp (each GPU renders 1/8 of the
@@ -191,6 +193,10 @@ def main():
                     help="only the timed region (profiling runs): no launch-alone, end-to-end or CPU legs")
     ap.add_argument("--cpu-budget", type=float, default=None, help="seconds of all-core CPU-baseline timing")
     ap.add_argument("--scene-global", action="store_true", help="read spheres from global memory, not LDS")
+    ap.add_argument("--exchange", choices=["remote", "rccl"], default="remote",
+                    help="N > 1 frame assembly: remote = each rank's render stores its finished pixels straight "
+                         "into rank 0's frame over xGMI (IPC-mapped, lrt_render_device_to_frame); rccl = pack to "
+                         "RGB, RCCL gather to rank 0, unshard kernel")
     ap.add_argument("--reserve-cus", type=int, default=None,
                     help="CUs the render stream leaves free for other streams (default 0)")
     ap.add_argument("--kernel", choices=["auto", "v0", "wf", "pool"], default="auto",
@@ -235,8 +241,8 @@ def main():
             dist.init_process_group(backend)
     import learnraytracing_amd as lrt
     from learnraytracing_amd import _lib as L
-    from learnraytracing_amd.dist import gather_to_root, max_shard_rows, shard_rows
-    from learnraytracing_amd.renderer import pack_rgb_tensor, unshard_rgb_tensor
+    from learnraytracing_amd.dist import SharedFrames, gather_to_root, max_shard_rows, shard_rows
+    from learnraytracing_amd.renderer import pack_rgb_tensor, render_tensor_to_frame, unshard_rgb_tensor
 
     lrt.InitializeTest()
     # --reserve-cus R: render on a CU-masked stream (lrt_stream_create) leaving R CUs to
@@ -264,12 +270,17 @@ def main():
     nslots = max(2, nstreams)
     bufs = [torch.zeros((max_rows, W, 4), dtype=torch.float32, device=dev) for _ in range(nslots)]
     rays = torch.zeros(1, dtype=torch.int64, device=dev)
-    # the exchange carries RGB only (lrt_pack_rgb): 12 of the 16 bytes per pixel cross xGMI
-    packed = [torch.empty((max_rows, W, 3), dtype=torch.float32, device=dev) if world > 1 else None
+    # remote exchange: rank 0's frames mapped into every rank; each render stores its finished
+    # pixels there itself (no pack, gather or unshard launch per step)
+    remote = world > 1 and args.exchange == "remote"
+    shared = SharedFrames(W, H, nslots, rank) if remote else None
+    gather_ex = world > 1 and not remote
+    # the RCCL exchange carries RGB only (lrt_pack_rgb): 12 of the 16 bytes per pixel cross xGMI
+    packed = [torch.empty((max_rows, W, 3), dtype=torch.float32, device=dev) if gather_ex else None
               for _ in range(nslots)]
-    gathered = [torch.empty((world, max_rows, W, 3), dtype=torch.float32, device=dev) if rank == 0 and world > 1
+    gathered = [torch.empty((world, max_rows, W, 3), dtype=torch.float32, device=dev) if rank == 0 and gather_ex
                 else None for _ in range(nslots)]
-    frames_out = [torch.empty((H, W, 4), dtype=torch.float32, device=dev) if rank == 0 and world > 1 else None
+    frames_out = [torch.empty((H, W, 4), dtype=torch.float32, device=dev) if rank == 0 and gather_ex else None
                   for _ in range(nslots)]
     stream = torch.cuda.current_stream(dev)
     # render streams (the first is the current stream); frame assembly and D2H on their own
@@ -283,7 +294,7 @@ def main():
         """Assemble slot's frame on rank 0 (after its gather), then optionally copy it to
         pinned host memory; the slot's next render waits for both."""
         done = None
-        if world > 1:
+        if gather_ex:
             done = torch.cuda.Event()
             with torch.cuda.stream(astream):
                 if work is not None:
@@ -294,7 +305,7 @@ def main():
         if d2h and rank == 0:
             cstream.wait_event(done if done is not None else rdone)
             with torch.cuda.stream(cstream):
-                host[slot].copy_(frames_out[slot] if world > 1 else bufs[slot], non_blocking=True)
+                host[slot].copy_(frames_out[slot] if gather_ex else bufs[slot], non_blocking=True)
             done = torch.cuda.Event()
             done.record(cstream)
         if done is not None:
@@ -303,13 +314,16 @@ def main():
     def step(k, d2h=False):
         slot = k % nslots
         rs = rstreams[k % nstreams]
-        lrt.render_tensor(job, bufs[slot], rays, rs)
+        if remote:
+            render_tensor_to_frame(job, bufs[slot], rays, shared.ptrs[slot], rs)
+        else:
+            lrt.render_tensor(job, bufs[slot], rays, rs)
         rdone = None
         if d2h and world == 1:
             rdone = torch.cuda.Event()
             rdone.record(rs)
         work = None
-        if world > 1:
+        if gather_ex:
             with torch.cuda.stream(rs):   # the gather is ordered after this step's render
                 pack_rgb_tensor(bufs[slot], packed[slot], rs)
                 _, work = gather_to_root(packed[slot], max_rows, world, rank, gathered=gathered[slot], async_op=True)
@@ -358,7 +372,10 @@ def main():
         scratch = torch.zeros(1, dtype=torch.int64, device=dev)
         for k in range(args.steps):
             ev[k][0].record(stream)
-            lrt.render_tensor(job, bufs[0], scratch, stream)
+            if remote:
+                render_tensor_to_frame(job, bufs[0], scratch, shared.ptrs[0], stream)
+            else:
+                lrt.render_tensor(job, bufs[0], scratch, stream)
             ev[k][1].record(stream)
         torch.cuda.synchronize()
         alone_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
@@ -366,18 +383,33 @@ def main():
             shape = (H, W, 4) if world > 1 else tuple(bufs[0].shape)   # --shard-of: the shard itself
             host = [torch.empty(shape, dtype=torch.float32, pin_memory=True) for _ in range(nslots)]
         e2e_steps = max(1, min(args.steps, 10))
-        for k in range(nslots):   # untimed: each pinned buffer's first copy maps its pages
-            step(k, d2h=True)
-        drain()
-        sync_all()
-        t2 = time.perf_counter()
-        for k in range(e2e_steps):
-            step(k, d2h=True)
-        drain()
-        torch.cuda.synchronize()
-        e2e_s = time.perf_counter() - t2
-        if world > 1:
+        if remote:   # a frame is complete once every rank's render of it is: barrier, then D2H
+            def e2e_step(k):
+                step(k)
+                sync_all()
+                if rank == 0:
+                    host[k % nslots].copy_(shared.tensor(k % nslots))
+            for k in range(nslots):
+                e2e_step(k)
+            sync_all()
+            t2 = time.perf_counter()
+            for k in range(e2e_steps):
+                e2e_step(k)
+            e2e_s = time.perf_counter() - t2
             dist.barrier()
+        else:
+            for k in range(nslots):   # untimed: each pinned buffer's first copy maps its pages
+                step(k, d2h=True)
+            drain()
+            sync_all()
+            t2 = time.perf_counter()
+            for k in range(e2e_steps):
+                step(k, d2h=True)
+            drain()
+            torch.cuda.synchronize()
+            e2e_s = time.perf_counter() - t2
+            if world > 1:
+                dist.barrier()
 
     stats = torch.tensor([elapsed, timed_rays, alone_ms or 0.0, e2e_s or 0.0], dtype=torch.float64,
                          device=dev if backend == "nccl" else "cpu")
@@ -447,7 +479,9 @@ def main():
                             + ("reference 9-sphere scene" if cfg["scene"] == "default" else "random_scene(1000, seed=1)"),
                 "width": W, "height": H, "spp_total": spp_total, "max_depth": D,
                 "rays_per_step": int(rays_per_step),
-                "parallelism": f"rows: row-block-cyclic x{world} (block {rb}), RCCL gather of RGB to rank 0"
+                "parallelism": f"rows: row-block-cyclic x{world} (block {rb}), "
+                               + ("each render stores its pixels into rank 0's frame over xGMI (IPC)" if remote
+                                  else "RCCL gather of RGB to rank 0")
                 if world > 1 else ("single GPU" if shards == 1 else
                                    f"DIAGNOSTIC: rank 0's shard of {shards} (block {rb}), no gather"),
                 "scene_reads": scene_reads(launch_info),
@@ -460,8 +494,10 @@ def main():
             "end_to_end": {
                 "value": round(total_rays / args.steps * e2e_steps / e2e_s / 1e6, 3), "unit": "Mray/s",
                 "ms_per_step": round(e2e_s / e2e_steps * 1e3, 4), "steps": e2e_steps,
-                "what": "render" + (" + RCCL gather + assembly" if world > 1 else "")
-                        + " + D2H of the RGBA frame into pinned host memory on rank 0, pipelined over 2 slots",
+                "what": "render" + ((" + remote stores into rank 0's frame, barrier" if remote else
+                                     " + RCCL gather + assembly") if world > 1 else "")
+                        + " + D2H of the RGBA frame into pinned host memory on rank 0"
+                        + (", one step at a time" if remote else ", pipelined over 2 slots"),
             } if e2e_s else None,
             "cpu_baseline": cpu,
             "cpu_baseline_1core": cpu1,
@@ -471,6 +507,12 @@ def main():
     if rstream is not None:
         torch.cuda.set_stream(torch.cuda.default_stream(dev))
         rstream.close()
+    if shared is not None:   # importers unmap first, then rank 0 frees
+        if rank != 0:
+            shared.close()
+        dist.barrier()
+        if rank == 0:
+            shared.close()
     lrt.ShutdownTest()
     if world > 1:
         dist.destroy_process_group()

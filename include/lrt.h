@@ -187,6 +187,25 @@ int lrt_default_scene(lrt_sphere* spheres, lrt_material* materials, int capacity
 int lrt_render_device(const lrt_render_desc* desc, float* d_backbuffer,
                       unsigned long long* d_rays, void* stream);
 
+/* lrt_render_device plus the multi-GPU frame exchange fused into the render: every finished
+ * pixel is also stored, as RGBA, into d_frame -- the whole width x height frame, row-major --
+ * at its global row (the row map above). d_frame may be another device's memory opened with
+ * lrt_ipc_open (one process per GPU) or peer-accessible memory: each rank's render writes its
+ * rows straight into rank 0's frame over xGMI, with no pack, gather or assembly launch; the
+ * frame is complete once every rank's render has completed (e.g. after a barrier). */
+int lrt_render_device_to_frame(const lrt_render_desc* desc, float* d_backbuffer,
+                               unsigned long long* d_rays, float* d_frame, void* stream);
+
+/* Device memory shareable across processes (hipIpc*) for that exchange: lrt_ipc_alloc makes a
+ * zeroed buffer of `bytes` on the first device and its handle (LRT_IPC_HANDLE_BYTES bytes, to
+ * send to the other processes); lrt_ipc_open maps a handle from another process (peer access
+ * enabled lazily); lrt_ipc_close unmaps it; lrt_ipc_free frees an lrt_ipc_alloc buffer. */
+#define LRT_IPC_HANDLE_BYTES 64
+int lrt_ipc_alloc(size_t bytes, void** d_ptr, void* handle);
+int lrt_ipc_free(void* d_ptr);
+int lrt_ipc_open(const void* handle, void** d_ptr);
+int lrt_ipc_close(void* d_ptr);
+
 /* Same on a HOST buffer: H2D of prev, render, D2H, blocking. *out_rays = counted rays. */
 int lrt_render_host(const lrt_render_desc* desc, float* backbuffer, long long* out_rays);
 

@@ -23,19 +23,29 @@ int main(int argc, char** argv) {
     float* backbuffer = new float[(size_t)w * h * 4];
     std::memset(backbuffer, 0, sizeof(float) * (size_t)w * h * 4);
     InitializeTest();                                                  // main.cpp:48
-    long long rays = 0;
-    double secs = 0.0;
+    long long rays = 0, steady_rays = 0;
+    double secs = 0.0, steady = 0.0;
     for (int f = 0; f < frames; ++f) {                                 // main.cpp:165
         int r = 0;
         const auto t0 = std::chrono::steady_clock::now();
         DrawTest(0.0f, f, w, h, backbuffer, r);
-        secs += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        secs += dt;
         rays += r;
+        if (f >= 2) {   // main.cpp:180 averages over more than 10 frames; the first two set up
+            steady += dt;
+            steady_rays += r;
+        }
     }
     ShutdownTest();                                                    // main.cpp:74
     const double s = secs / frames;                                    // main.cpp:188-189
     std::printf("%.2fms (%.1f FPS) %.1fMrays/s %.2fMrays/frame frames %i rays %lld\n", s * 1000.0, 1.0 / s,
                 (double)rays / frames / s * 1.0e-6, (double)rays / frames * 1.0e-6, frames, rays);
+    if (frames > 2) {
+        const double ss = steady / (frames - 2);
+        std::printf("steady %.3fms (%.1f FPS) %.1fMrays/s over frames 2..%i\n", ss * 1000.0, 1.0 / ss,
+                    (double)steady_rays / steady * 1.0e-6, frames - 1);
+    }
     FILE* fp = std::fopen(argv[4], "wb");
     if (!fp) return 1;
     std::fprintf(fp, "PF\n%d %d\n-1.0\n", w, h);   // linear RGB, bottom row first (the backbuffer's order)

@@ -35,6 +35,7 @@ F_V3 = 128          # removed in round 3: rejected with LRT_E_INVALID
 F_WAVEFRONT = 256
 F_POOL = 512
 DEV_PEER_COPY = 1   # lrt_initialize_devices: gather by device-to-device copies, not RCCL
+IPC_HANDLE_BYTES = 64
 
 
 class LrtError(RuntimeError):
@@ -110,6 +111,11 @@ SIGNATURES = {
     "lrt_set_scene": (_i, [_c.POINTER(Sphere), _c.POINTER(Material), _i]),
     "lrt_default_scene": (_i, [_c.POINTER(Sphere), _c.POINTER(Material), _i, _c.POINTER(_i)]),
     "lrt_render_device": (_i, [_c.POINTER(RenderDesc), _vp, _vp, _vp]),
+    "lrt_render_device_to_frame": (_i, [_c.POINTER(RenderDesc), _vp, _vp, _vp, _vp]),
+    "lrt_ipc_alloc": (_i, [_c.c_size_t, _c.POINTER(_vp), _vp]),
+    "lrt_ipc_free": (_i, [_vp]),
+    "lrt_ipc_open": (_i, [_vp, _c.POINTER(_vp)]),
+    "lrt_ipc_close": (_i, [_vp]),
     "lrt_render_host": (_i, [_c.POINTER(RenderDesc), _vp, _c.POINTER(_c.c_longlong)]),
     "lrt_render_device_ex": (_i, [_c.POINTER(RenderDesc), _vp, _vp, _c.POINTER(Features), _vp]),
     "lrt_render_host_ex": (_i, [_c.POINTER(RenderDesc), _vp, _c.POINTER(_c.c_longlong), _c.POINTER(Features)]),

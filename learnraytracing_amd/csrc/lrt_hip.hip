@@ -95,7 +95,14 @@ struct KernelArgs {
     const int* perm;              // v5: queue position -> tile, heaviest measured tiles first (null: identity)
     unsigned* tcost;              // v5: per-tile cost recording (100 MHz ticks of the tile's wave), or null
     int sampOnly;                 // colours only (the pipelined host path): samp is the caller's
+    float4* frame;                // lrt_render_device_to_frame: the whole width x height frame (any
+                                  // device, IPC/peer-mapped) that each finished pixel is also stored
+                                  // to at its global row -- the multi-GPU exchange fused into the
+                                  // render's last store; null otherwise
 };
+
+// Global position of local row ly (lrt_render_desc's row map).
+LRT_DEV int GlobalRow(const KernelArgs& a, int ly) { return a.y0 + (ly / a.rb) * a.rb * a.rp + a.rph * a.rb + ly % a.rb; }
 constexpr int kLerpTable = 1 << 16;
 constexpr int kFixedSpheres = 9;   // the reference's kSphereCount (parallel.cpp:27)
 
@@ -329,7 +336,10 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
             }
             if (kSplit > 1) __builtin_amdgcn_wave_barrier();
         }
-        if (!kSamp && valid && sub == 0) *px = acc;
+        if (!kSamp && valid && sub == 0) {
+            *px = acc;
+            if (a.frame) a.frame[(size_t)y * a.width + x] = acc;   // the frame exchange, fused
+        }
         if constexpr (kFeat) {
 #pragma unroll
             for (int k = 0; k < 6; ++k)
@@ -382,9 +392,11 @@ namespace lrt {
 
 
 // Sample mode's second half: TraceRowJob's progressive lerp (parallel.cpp:262,280-286)
-// over the frame planes in order, one thread per pixel (coalesced plane reads).
+// over the frame planes in order, one thread per pixel (coalesced plane reads). `a` supplies
+// the window's row map and the fused-exchange frame (a.frame); pixel i is the window's
+// pixel pix0 + i.
 __global__ void merge_samples_kernel(const float4* __restrict__ samp, float4* __restrict__ out, const float* lerp,
-                                     int npix, int frame0, int frames, size_t stride) {
+                                     int npix, int frame0, int frames, size_t stride, const KernelArgs a, int pix0) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= npix) return;
     const float4 o = out[i];
@@ -399,6 +411,10 @@ __global__ void merge_samples_kernel(const float4* __restrict__ samp, float4* __
     d[0] = acc.x;
     d[1] = acc.y;
     d[2] = acc.z;
+    if (a.frame) {   // the frame exchange, fused
+        const int p = pix0 + i, lx = p % a.xc, ly = p / a.xc;
+        a.frame[(size_t)GlobalRow(a, ly) * a.width + a.x0 + lx] = make_float4(acc.x, acc.y, acc.z, o.w);
+    }
 }
 
 // The pipelined host path's lerp (render_host_pipelined): prev from device memory (copied
@@ -1154,7 +1170,7 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
             e = hipGetLastError();
             if (e != hipSuccess) return hip_fail(e, "trace_kernel (samples) launch");
             merge_samples_kernel<<<(unsigned)((npix + 255) / 256), 256, 0, s>>>(a.samp, a.out, a.lerp, (int)npix,
-                                                                               a.frame0, a.frames, npix);
+                                                                               a.frame0, a.frames, npix, a, 0);
             e = hipGetLastError();
             if (e != hipSuccess) return hip_fail(e, "merge_samples_kernel launch");
             e = hipFreeAsync(a.samp, s);
@@ -1550,7 +1566,7 @@ int launch_wavefront(KernelArgs a, bool lds, hipStream_t s) {
             }
         }
         merge_samples_kernel<<<(unsigned)((cp + 255) / 256), 256, 0, s>>>(w.samp, a.out + pix0, a.lerp, (int)cp,
-                                                                         a.frame0, a.frames, cp);
+                                                                         a.frame0, a.frames, cp, a, (int)pix0);
         e = hipGetLastError();
         if (e != hipSuccess) return hip_fail(e, "wavefront launch");
     }
@@ -1565,8 +1581,10 @@ int auto_kernel(const KernelArgs& a, const lrt_render_desc* d, bool feat);
 
 // colours_out (render_host's pipeline): no lerp -- frame f's sample colours go to plane
 // f - frame0 of colours_out (x_count * row_count float4 each) and d_buf is not touched.
+// frame (lrt_render_device_to_frame): every finished pixel is stored there too, at its global
+// row -- the whole width x height RGBA frame, possibly another device's memory.
 int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_rays, const lrt_features* feat,
-                  hipStream_t s, float4* colours_out = nullptr) {
+                  hipStream_t s, float4* colours_out = nullptr, float* frame = nullptr) {
     int rc = validate(d);
     if (rc) return rc;
     if (!ctx().ready) return fail(LRT_E_STATE, "lrt_initialize() has not been called");
@@ -1636,6 +1654,9 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     a.tcost = nullptr;
     a.samp = colours_out;
     a.sampOnly = colours_out ? 1 : 0;
+    a.frame = reinterpret_cast<float4*>(frame);
+    if (frame && (want_feat || colours_out))
+        return fail(LRT_E_INVALID, "a frame destination is for plain renders (no features, no colours-only)");
     if (colours_out) {   // v0, one frame lane per pixel, sample mode
         if (want_feat || !lds || a.bv.on) return fail(LRT_E_INVALID, "colours-only render: LDS linear-scan scenes only");
         if (d->max_depth <= 8) return launch_depth<8, 1>(a, lds, d->x_count, d->row_count, s);
@@ -2412,6 +2433,56 @@ int lrt_render_device(const lrt_render_desc* desc, float* d_backbuffer, unsigned
     std::lock_guard<std::mutex> lk(g_mu);
     DeviceScope ds_(0);   // context 0's device (device 0 of lrt_initialize_devices)
     return render_device(desc, d_backbuffer, d_rays, nullptr, (hipStream_t)stream);
+}
+
+int lrt_render_device_to_frame(const lrt_render_desc* desc, float* d_backbuffer, unsigned long long* d_rays,
+                               float* d_frame, void* stream) {
+    RoctxRange rr_("lrt_render_device_to_frame");
+    std::lock_guard<std::mutex> lk(g_mu);
+    DeviceScope ds_(0);
+    if (!d_frame) return fail(LRT_E_INVALID, "d_frame is NULL");
+    return render_device(desc, d_backbuffer, d_rays, nullptr, (hipStream_t)stream, nullptr, d_frame);
+}
+
+int lrt_ipc_alloc(size_t bytes, void** d_ptr, void* handle) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    DeviceScope ds_(0);
+    if (!d_ptr || !handle || bytes == 0) return fail(LRT_E_INVALID, "invalid ipc alloc arguments");
+    *d_ptr = nullptr;
+    LRT_HIP(hipMalloc(d_ptr, bytes));   // its own allocation: the handle maps exactly this buffer
+    LRT_HIP(hipMemset(*d_ptr, 0, bytes));
+    hipIpcMemHandle_t h;
+    const hipError_t e = hipIpcGetMemHandle(&h, *d_ptr);
+    if (e != hipSuccess) {
+        (void)hipFree(*d_ptr);
+        *d_ptr = nullptr;
+        return hip_fail(e, "hipIpcGetMemHandle");
+    }
+    static_assert(sizeof(h) <= LRT_IPC_HANDLE_BYTES, "IPC handle size");
+    memcpy(handle, &h, sizeof(h));
+    return LRT_OK;
+}
+
+int lrt_ipc_free(void* d_ptr) {
+    if (!d_ptr) return LRT_OK;
+    LRT_HIP(hipFree(d_ptr));
+    return LRT_OK;
+}
+
+int lrt_ipc_open(const void* handle, void** d_ptr) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    DeviceScope ds_(0);
+    if (!handle || !d_ptr) return fail(LRT_E_INVALID, "invalid ipc open arguments");
+    hipIpcMemHandle_t h;
+    memcpy(&h, handle, sizeof(h));
+    LRT_HIP(hipIpcOpenMemHandle(d_ptr, h, hipIpcMemLazyEnablePeerAccess));
+    return LRT_OK;
+}
+
+int lrt_ipc_close(void* d_ptr) {
+    if (!d_ptr) return LRT_OK;
+    LRT_HIP(hipIpcCloseMemHandle(d_ptr));
+    return LRT_OK;
 }
 
 int lrt_render_device_ex(const lrt_render_desc* desc, float* d_backbuffer, unsigned long long* d_rays,

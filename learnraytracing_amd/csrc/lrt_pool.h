@@ -301,6 +301,7 @@ __global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const Ker
                     acc.y = c3.y;
                     acc.z = c3.z;
                     *mpx = acc;   // alpha as read
+                    if (a.frame) a.frame[(size_t)GlobalRow(a, my) * a.width + a.x0 + mx] = acc;   // the exchange, fused
                 }
             }
             // the next round overwrites the slots: every read above completes first

@@ -10,6 +10,10 @@ G and row_block (tests/test_gpu_parity.py, tests/test_dist_cpu.py).
 
 The collective is torch.distributed (backend "nccl" = RCCL on ROCm; "gloo" on CPU
 for tests). The reference has no distributed code at all.
+
+SharedFrames is the other exchange: rank 0's frames are mapped into every rank over IPC and
+each rank's render stores its finished pixels straight into them (xGMI writes from the render
+kernel, lrt_render_device_to_frame) -- no pack, gather or assembly launch per step.
 """
 from __future__ import annotations
 
@@ -71,3 +75,68 @@ def gather_to_root(local, max_rows: int, world: int, rank: int, gathered=None, g
     if stage and rank == 0:
         gathered.copy_(recv)
     return gathered, work
+
+
+class SharedFrames:
+    """`count` RGBA frames (height x width) allocated on rank 0 (lrt_ipc_alloc) and mapped into
+    every other rank (lrt_ipc_open, peer access over xGMI), for the fused exchange: rank r's
+    render writes its rows into rank 0's frame directly. `ptrs[i]` is frame i's device address
+    in this process; rank 0 can view frame i as a tensor with `tensor(i)`."""
+
+    def __init__(self, width: int, height: int, count: int, rank: int, group=None):
+        import ctypes
+        import torch.distributed as dist
+
+        from . import _lib as L
+        self.width, self.height, self.count, self.rank = width, height, count, rank
+        self.bytes = width * height * 16
+        self._owned, self._opened, self.ptrs = [], [], []
+        handles = None
+        if rank == 0:
+            handles = []
+            for _ in range(count):
+                p = ctypes.c_void_p()
+                h = (ctypes.c_char * L.IPC_HANDLE_BYTES)()
+                L.check(L.lib().lrt_ipc_alloc(self.bytes, ctypes.byref(p), ctypes.cast(h, ctypes.c_void_p)))
+                self._owned.append(p.value)
+                handles.append(bytes(h))
+            self.ptrs = list(self._owned)
+        box = [handles]
+        if dist.is_initialized():
+            dist.broadcast_object_list(box, src=0, group=group)
+        if rank != 0:
+            for hb in box[0]:
+                h = (ctypes.c_char * L.IPC_HANDLE_BYTES).from_buffer_copy(hb)
+                p = ctypes.c_void_p()
+                L.check(L.lib().lrt_ipc_open(ctypes.cast(h, ctypes.c_void_p), ctypes.byref(p)))
+                self._opened.append(p.value)
+            self.ptrs = list(self._opened)
+
+    def tensor(self, i: int):
+        """Frame i as a (height, width, 4) float32 cuda tensor over rank 0's own memory (no copy)."""
+        if self.rank != 0:
+            raise ValueError("only rank 0 owns the frames")
+        return _tensor_from_ptr(self.ptrs[i], (self.height, self.width, 4))
+
+    def close(self) -> None:
+        import ctypes
+
+        from . import _lib as L
+        for p in self._opened:
+            L.lib().lrt_ipc_close(ctypes.c_void_p(p))
+        for p in self._owned:
+            L.lib().lrt_ipc_free(ctypes.c_void_p(p))
+        self._opened, self._owned, self.ptrs = [], [], []
+
+
+class _CudaArray:
+    """__cuda_array_interface__ of float32 device memory, for torch.as_tensor (no copy)."""
+
+    def __init__(self, ptr: int, shape):
+        self.__cuda_array_interface__ = {"shape": tuple(shape), "typestr": "<f4", "data": (int(ptr), False),
+                                         "version": 3, "strides": None}
+
+
+def _tensor_from_ptr(ptr: int, shape):
+    import torch
+    return torch.as_tensor(_CudaArray(ptr, shape), device="cuda")

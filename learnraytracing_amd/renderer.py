@@ -228,6 +228,24 @@ def render_tensor(job: Job, buf, rays, stream=None) -> None:
                                       ctypes.c_void_p(rays.data_ptr()), ctypes.c_void_p(s.cuda_stream)))
 
 
+def render_tensor_to_frame(job: Job, buf, rays, frame_ptr: int, stream=None) -> None:
+    """render_tensor plus the fused frame exchange (lrt_render_device_to_frame): each finished
+    pixel is also stored into the width x height RGBA frame at frame_ptr (a device pointer,
+    e.g. rank 0's frame opened over IPC) at its global row."""
+    import torch
+
+    d = job.desc()
+    need = d.row_count * d.x_count * 4
+    if not (buf.is_cuda and buf.dtype == torch.float32 and buf.is_contiguous() and buf.numel() >= need):
+        raise L.LrtError(L.LRT_E_INVALID, f"buf must be a contiguous cuda float32 tensor of >= {need} elements")
+    if not (rays.is_cuda and rays.dtype == torch.int64 and rays.numel() >= 1):
+        raise L.LrtError(L.LRT_E_INVALID, "rays must be a cuda int64 tensor")
+    s = stream if stream is not None else torch.cuda.current_stream(buf.device)
+    L.check(L.lib().lrt_render_device_to_frame(ctypes.byref(d), ctypes.c_void_p(buf.data_ptr()),
+                                               ctypes.c_void_p(rays.data_ptr()), ctypes.c_void_p(int(frame_ptr)),
+                                               ctypes.c_void_p(s.cuda_stream)))
+
+
 class RenderStream:
     """A CU-masked render stream (lrt_stream_create) leaving `reserved_cus` CUs free for
     concurrent work such as RCCL collectives; `.torch` is the torch.cuda.ExternalStream."""

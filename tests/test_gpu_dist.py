@@ -85,6 +85,59 @@ def test_two_rank_gpu_shards_assemble_bitwise(gpu, tmp_path, world, rb, frames):
     assert int(np.load(tmp_path / "rays.npy")[0]) == want_rays
 
 
+def _remote_worker(rank, world, port, w, h, rb, frames, depth, outdir):
+    """The fused exchange: rank 0's frame is mapped into every rank over IPC and each rank's
+    render stores its finished pixels into it (lrt_render_device_to_frame)."""
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import learnraytracing_amd as lrt
+    from learnraytracing_amd.dist import SharedFrames, max_shard_rows
+    from learnraytracing_amd.renderer import render_tensor_to_frame
+    lrt.InitializeTest()
+    shared = None
+    try:
+        shared = SharedFrames(w, h, 1, rank)
+        local = torch.zeros((max_shard_rows(h, rb, world), w, 4), dtype=torch.float32, device="cuda")
+        rays = torch.zeros(1, dtype=torch.int64, device="cuda")
+        job = lrt.Job(width=w, height=h, frames=frames, max_depth=depth, row_block=rb, row_period=world,
+                      row_phase=rank)
+        render_tensor_to_frame(job, local, rays, shared.ptrs[0])
+        torch.cuda.synchronize()
+        dist.barrier()   # every rank's render has completed: the frame is assembled
+        tot = rays.cpu()
+        dist.all_reduce(tot)
+        if rank == 0:
+            np.save(os.path.join(outdir, "frame.npy"), shared.tensor(0).cpu().numpy())
+            np.save(os.path.join(outdir, "rays.npy"), tot.numpy())
+        if rank != 0:
+            shared.close()
+        dist.barrier()
+    finally:
+        if shared is not None and rank == 0:
+            shared.close()
+        lrt.ShutdownTest()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,rb,frames", [(2, 8, 4), (3, 5, 32)])
+def test_remote_store_exchange_assembles_bitwise(gpu, tmp_path, world, rb, frames):
+    """Ranks sharing GPU 0 (gloo for the control plane) write their rows straight into rank 0's
+    IPC-mapped frame from the render kernel: the frame equals a one-rank render bit for bit."""
+    import torch.multiprocessing as mp
+    w, h, depth = 256, 144, 8
+    mp.start_processes(_remote_worker, args=(world, _free_port(), w, h, rb, frames, depth, str(tmp_path)),
+                       nprocs=world, start_method="spawn", join=True)
+    frame = np.load(tmp_path / "frame.npy")
+    want = np.zeros((h, w, 4), np.float32)
+    want_rays = gpu.render_host(gpu.Job(width=w, height=h, frames=frames, max_depth=depth), want)
+    assert np.array_equal(frame[..., :3].view(np.uint32), want[..., :3].view(np.uint32))
+    assert int(np.load(tmp_path / "rays.npy")[0]) == want_rays
+
+
 def test_one_rank_rccl_gather_assembles_bitwise(gpu, tmp_path):
     """The RCCL path itself: a one-rank "nccl" (RCCL) process group, where gather_to_root
     still issues dist.gather (RCCL moves the device shard into rank 0's gathered buffer),
@@ -102,15 +155,15 @@ def test_one_rank_rccl_gather_assembles_bitwise(gpu, tmp_path):
     assert int(np.load(tmp_path / "rays.npy")[0]) == want_rays
 
 
-@pytest.mark.parametrize("scaling", ["strong", "weak"])
-def test_bench_two_ranks_gloo(gpu, scaling):
+@pytest.mark.parametrize("scaling,exchange", [("strong", "remote"), ("weak", "remote"), ("strong", "rccl")])
+def test_bench_two_ranks_gloo(gpu, scaling, exchange):
     """bench.py --gpus 2 over gloo on one GPU: one JSON line from rank 0 with the
     aggregate of both ranks. Strong scaling (the default) renders config 2's own frame
     (4 spp over the two row shards: exactly the 1-GPU ray count); weak renders 8 spp."""
     env = dict(os.environ, LRT_DIST_BACKEND="gloo")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "3", "--warmup", "1", "--scaling", scaling]
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--scaling", scaling, "--exchange", exchange]
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]

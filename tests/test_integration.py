@@ -56,11 +56,12 @@ def _read_pfm(path):
         return np.frombuffer(f.read(), "<f4").reshape(h, w, 3)
 
 
-def _run_host(exe, w, h, frames, tmp_path):
+def _run_host(exe, w, h, frames, tmp_path, env=None):
     if not os.path.exists(exe):
         pytest.skip(f"{os.path.relpath(exe, ROOT)} not built (build() makes it where the reference is present)")
     out = tmp_path / "out.pfm"
-    p = subprocess.run([exe, str(w), str(h), str(frames), str(out)], capture_output=True, text=True, timeout=120)
+    p = subprocess.run([exe, str(w), str(h), str(frames), str(out)], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, **(env or {})))
     assert p.returncode == 0, p.stderr[-2000:]
     rays = int(re.search(r"rays (\d+)", p.stdout).group(1))
     return _read_pfm(out), rays
@@ -81,6 +82,20 @@ def _drawtest_oracle(w, h, frames):
 def test_headless_host_matches_oracle(exe, tmp_path):
     w, h, frames = 160, 90, 3
     img, rays = _run_host(exe, w, h, frames, tmp_path)
+    want, wrays = _drawtest_oracle(w, h, frames)
+    assert rays == wrays
+    assert np.array_equal(img.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", ["0", "0,0,0"], ids=["rccl-1", "copy-3"])
+def test_binding_multi_device_matches_oracle(devices, tmp_path):
+    """The unchanged main.cpp-style host through parallel_lrt.cpp with LRT_DEVICES: DrawTest's
+    rows split over the listed devices (lrt_initialize_devices; RCCL with one device here, the
+    copy exchange for a repeated id) -- the same bits as the oracle."""
+    w, h, frames = 160, 90, 3
+    img, rays = _run_host(os.path.join(ROOT, "integration", "_build", "drawtest_ref_api"), w, h, frames, tmp_path,
+                          env={"LRT_DEVICES": devices})
     want, wrays = _drawtest_oracle(w, h, frames)
     assert rays == wrays
     assert np.array_equal(img.view(np.uint32), want.view(np.uint32))
