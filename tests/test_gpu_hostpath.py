@@ -44,9 +44,10 @@ print("ok")
     ({"LRT_HOST_CHUNKS": "1"}, True, 160, 90),
     ({"LRT_HOST_CHUNKS": "3"}, True, 200, 117),          # uneven chunks
     ({"LRT_HOST_CHUNKS": "8"}, True, 96, 61),
+    ({"LRT_DRAW_LOOKAHEAD": "0"}, True, 200, 117),      # no look-ahead render of the next frame
     ({"LRT_HOST_PIPELINE": "0"}, True, 200, 117),        # zero copy
     ({}, False, 200, 117),                               # pageable: staged
-], ids=["pipe2", "pipe1", "pipe3", "pipe8", "zerocopy", "pageable"])
+], ids=["pipe2", "pipe1", "pipe3", "pipe8", "nolookahead", "zerocopy", "pageable"])
 def test_drawtest_host_paths(env, pinned, w, h):
     code = SCRIPT.format(root=ROOT, oracle=os.path.join(ROOT, "oracle"), w=w, h=h, pinned=pinned)
     p = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), capture_output=True, text=True,

@@ -234,3 +234,41 @@ def test_config3_full_frame_vs_oracle(gpu):
     want, wrays = oracle.orc_render(1920, 1080, 16, 50)
     _bitwise(buf, want, "config 3 full frame")
     assert rays == wrays
+
+
+def test_drawtest_lookahead_hits_and_misses(gpu):
+    """lrt_draw_test renders frame f + 1's colours behind call f: DrawTest's colours depend on
+    frameCount, the size and the scene only (parallel.cpp:297-323; `time` is unused) and
+    main.cpp:165,187 asks for frameCount + 1 next. A call continuing the sequence uses them
+    (lookahead=hit); a repeated or skipped frame, a new size or a new scene renders for itself
+    (miss). The oracle's bits and ray counts either way."""
+    from learnraytracing_amd import _lib as L
+    from learnraytracing_amd.scene import scene_arrays
+
+    def run(seq, w, h, bb, want, spheres=None, mats=None):
+        for f, expect in seq:
+            rays = gpu.DrawTest(0.0, f, w, h, bb)
+            ll = L.last_launch()
+            assert ll.get("host") == "pipelined" and ll.get("lookahead") == expect, (f, ll)
+            _, wr = oracle.orc_render(w, h, 1, 20, frame0=f, buf=want, spheres=spheres, mats=mats)
+            assert rays == wr, (f, rays, wr)
+            _bitwise(bb.reshape(h, w, 4), want, f"frame {f} ({expect})")
+
+    w, h = 320, 180
+    bb = gpu.pinned_backbuffer(w * h * 4)
+    bb[:] = 0.0
+    want = np.zeros((h, w, 4), np.float32)
+    run([(0, "miss"), (1, "hit"), (2, "hit"), (2, "miss"), (3, "hit"), (7, "miss"), (8, "hit")], w, h, bb, want)
+    w2, h2 = 200, 117   # a new size: its own look-ahead
+    bb2 = gpu.pinned_backbuffer(w2 * h2 * 4)
+    bb2[:] = 0.0
+    want2 = np.zeros((h2, w2, 4), np.float32)
+    run([(9, "miss"), (10, "hit")], w2, h2, bb2, want2)
+    sph, mats = gpu.default_scene()
+    sph[2].center = L.f3(sph[2].center.x + 0.25, sph[2].center.y, sph[2].center.z)
+    gpu.set_scene(sph, mats)   # a new scene between frames 10 and 11: the look-ahead is stale
+    try:
+        s, m = scene_arrays(sph, mats)
+        run([(11, "miss"), (12, "hit")], w2, h2, bb2, want2, spheres=s, mats=m)
+    finally:
+        gpu.set_scene(*gpu.default_scene())
