@@ -425,17 +425,17 @@ __global__ __launch_bounds__(256) void merge_to_host_kernel(const float4* __rest
                                                             const float4* __restrict__ prev, float4* host,
                                                             const float* lerp, int npix, int frame0, int frames,
                                                             size_t stride) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= npix) return;
-    const float4 o = prev[i];
-    F3 acc = f3(o.x, o.y, o.z);
-    for (int k = 0; k < frames; ++k) {   // parallel.cpp:262,282 in frame order
-        const float4 c = samp[(size_t)k * stride + i];
-        const int f = frame0 + k;
-        const float lerpFac = f < kLerpTable ? lerp[f] : (float)f / (float)(f + 1);
-        acc = acc * lerpFac + f3(c.x, c.y, c.z) * (1.0f - lerpFac);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < npix; i += gridDim.x * blockDim.x) {
+        const float4 o = prev[i];
+        F3 acc = f3(o.x, o.y, o.z);
+        for (int k = 0; k < frames; ++k) {   // parallel.cpp:262,282 in frame order
+            const float4 c = samp[(size_t)k * stride + i];
+            const int f = frame0 + k;
+            const float lerpFac = f < kLerpTable ? lerp[f] : (float)f / (float)(f + 1);
+            acc = acc * lerpFac + f3(c.x, c.y, c.z) * (1.0f - lerpFac);
+        }
+        host[i] = make_float4(acc.x, acc.y, acc.z, o.w);   // alpha as read
     }
-    host[i] = make_float4(acc.x, acc.y, acc.z, o.w);   // alpha as read
 }
 
 }  // namespace lrt
@@ -537,11 +537,16 @@ struct Context {
         uint64_t sig = 0;              // the render signature (geometry, camera, scene)
         uint64_t gkey = 0;             // its geometry only: views that can share an order
         long long ntiles = 0, cap = 0;
-        int state = 0;                 // 0: free, 1: costs being recorded, 2: permutation ready
-        unsigned* d_cost = nullptr;
-        int* d_perm = nullptr;         // written once (state 1 -> 2), read by every later launch
-        hipEvent_t ev_rec = nullptr;   // the recording launch's end
-        int donor = -1;                // state 1: the entry whose ready order launches borrow meanwhile
+        int state = 0;                 // 0: free, 2: permutation ready once ev_rec has passed
+        void* d_base = nullptr;        // one allocation: cost, sorted keys, tile ids, perm, sort scratch
+        unsigned* d_cost = nullptr;    // written by the recording launch
+        unsigned* d_keys = nullptr;
+        int* d_ids = nullptr;          // 0..cap-1
+        int* d_perm = nullptr;         // written once (by the sort), read by every later launch
+        void* d_tmp = nullptr;
+        size_t tmp_bytes = 0;
+        hipEvent_t ev_rec = nullptr;   // after the recording launch and the sort behind it
+        int donor = -1;                // the entry whose order the recording launch borrowed
         // the streams whose launches read d_perm / wrote d_cost, each with an event after its
         // last such launch: the entry is reused only once all of them have passed it
         std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
@@ -579,9 +584,13 @@ struct Context {
         bool on = false;
         lrt_render_desc d;            // the render they are (memcmp: descs are zero-filled)
         unsigned scene_version = 0;
-        float4* col = nullptr;
-        size_t bytes = 0;
-        unsigned long long* d_rays = nullptr;
+        int cur = 0;                  // the buffer pair holding them (the other is free)
+        float4* col[2] = {};
+        size_t bytes[2] = {};
+        unsigned long long* d_rays = nullptr;   // 2 counters
+        hipStream_t stream = nullptr;  // CU-masked: leaves CUs for the lerps it runs beside
+        hipEvent_t ev = nullptr;       // recorded after the look-ahead render
+        hipEvent_t ev_render = nullptr;
     } ahead;
     float* d_feat[6] = {};      // lrt_render_host_ex feature staging
     size_t feat_bytes[6] = {};
@@ -1293,7 +1302,39 @@ int order_used(Context::TileOrder& e, hipStream_t s) {
 }
 // Picks a's order for this launch: a.perm (null: queue order) and, for the recording launch,
 // a.tcost. *users gets the entries whose buffers the launch touches (order_used after it).
-int tile_order(KernelArgs& a, int kPix, long long ntiles, bool& record, Context::TileOrder* users[2]) {
+hipError_t sort_tiles_desc(const unsigned* cost_in, unsigned* keys_out, const int* ids_in, int* perm_out, int n,
+                           void* tmp, size_t* tmp_bytes, hipStream_t s);   // lrt_sort.hip
+hipError_t fill_iota(int* v, int n, hipStream_t s);
+
+// Sizes entry e for ntiles tiles (at least 65,536, so views of other sizes rarely reallocate).
+// Entries are allocated together on first use, so a new view's first launch does not wait
+// for hipMalloc.
+int order_alloc(Context::TileOrder& e, long long ntiles, hipStream_t s) {
+    if (e.cap >= ntiles) return LRT_OK;
+    const long long cap = std::max(ntiles, 65536LL);
+    size_t tmp = 0;
+    LRT_HIP(sort_tiles_desc(nullptr, nullptr, nullptr, nullptr, (int)cap, nullptr, &tmp, s));
+    const size_t arr = ((size_t)cap * 4 + 255) & ~(size_t)255;
+    if (e.d_base) (void)hipFree(e.d_base);   // (its launches have passed: order_release)
+    e.d_base = nullptr;
+    e.cap = 0;
+    if (hipMalloc(&e.d_base, 4 * arr + tmp) != hipSuccess) {
+        e.d_base = nullptr;
+        return fail(LRT_E_NOMEM, "hipMalloc(tile order)");
+    }
+    char* b = static_cast<char*>(e.d_base);
+    e.d_cost = reinterpret_cast<unsigned*>(b);
+    e.d_keys = reinterpret_cast<unsigned*>(b + arr);
+    e.d_ids = reinterpret_cast<int*>(b + 2 * arr);
+    e.d_perm = reinterpret_cast<int*>(b + 3 * arr);
+    e.d_tmp = b + 4 * arr;
+    e.tmp_bytes = tmp;
+    LRT_HIP(fill_iota(e.d_ids, (int)cap, s));
+    e.cap = cap;
+    return LRT_OK;
+}
+
+int tile_order(KernelArgs& a, int kPix, long long ntiles, bool& record, Context::TileOrder* users[2], hipStream_t s) {
     record = false;
     users[0] = users[1] = nullptr;
     if (!pool_order_on() || ntiles < 2 * kV0Queues) return LRT_OK;
@@ -1329,47 +1370,30 @@ int tile_order(KernelArgs& a, int kPix, long long ntiles, bool& record, Context:
                 if (o.donor == (int)(e - c.order)) o.donor = -1;
         }
         if (e->cap < ntiles) {
-            if (e->d_cost) (void)hipFree(e->d_cost);
-            if (e->d_perm) (void)hipFree(e->d_perm);
-            e->d_cost = nullptr;
-            e->d_perm = nullptr;
-            e->cap = 0;
             e->state = 0;
-            if (hipMalloc(&e->d_cost, sizeof(unsigned) * ntiles) != hipSuccess ||
-                hipMalloc(&e->d_perm, sizeof(int) * ntiles) != hipSuccess)
-                return fail(LRT_E_NOMEM, "hipMalloc(tile order)");
-            e->cap = ntiles;
+            for (auto& o : c.order)   // the first use sizes every unallocated entry at once
+                if (&o == e || (o.cap == 0 && o.state == 0))
+                    if (int rc = order_alloc(o, ntiles, s)) return rc;
         }
         if (!e->ev_rec) LRT_HIP(hipEventCreateWithFlags(&e->ev_rec, hipEventDisableTiming));
         e->sig = sig;
         e->gkey = gkey;
         e->ntiles = ntiles;
-        e->state = 1;
+        // the recording launch writes d_cost and the sort behind it (launch_pool) d_perm:
+        // ready for every later launch once ev_rec has passed, which each of them waits for
+        e->state = 2;
         e->donor = donor;
         a.tcost = e->d_cost;
         record = true;
-    } else if (e->state == 1) {
-        const hipError_t q = hipEventQuery(e->ev_rec);
-        if (q != hipSuccess && q != hipErrorNotReady) return hip_fail(q, "hipEventQuery(tile costs)");
-        if (q == hipSuccess) {   // the costs are in: sort them (once per signature)
-            std::vector<unsigned> cost((size_t)ntiles);
-            LRT_HIP(hipMemcpy(cost.data(), e->d_cost, sizeof(unsigned) * ntiles, hipMemcpyDeviceToHost));
-            std::vector<int> perm((size_t)ntiles);
-            for (long long i = 0; i < ntiles; ++i) perm[(size_t)i] = (int)i;
-            std::stable_sort(perm.begin(), perm.end(), [&](int x, int y) { return cost[(size_t)x] > cost[(size_t)y]; });
-            // blocking: the permutation is in device memory before ANY stream's launch reads
-            // it (no launch has read this entry's d_perm yet)
-            LRT_HIP(hipMemcpy(e->d_perm, perm.data(), sizeof(int) * ntiles, hipMemcpyHostToDevice));
-            e->state = 2;
-            e->donor = -1;
+        if (donor >= 0) {   // meanwhile the newest order of the same geometry
+            users[1] = &c.order[donor];
+            LRT_HIP(hipStreamWaitEvent(s, users[1]->ev_rec, 0));
+            a.perm = users[1]->d_perm;
+            users[1]->tick = ++c.order_tick;
         }
-    }
-    if (e->state == 2) {
+    } else {
+        LRT_HIP(hipStreamWaitEvent(s, e->ev_rec, 0));
         a.perm = e->d_perm;
-    } else if (e->donor >= 0) {
-        users[1] = &c.order[e->donor];
-        a.perm = users[1]->d_perm;
-        users[1]->tick = ++c.order_tick;
     }
     users[0] = e;
     e->tick = ++c.order_tick;
@@ -1432,7 +1456,7 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
 #endif
     bool record = false;
     Context::TileOrder* users[2];
-    if (int rc = tile_order(a, kPix, ntiles, record, users)) return rc;
+    if (int rc = tile_order(a, kPix, ntiles, record, users, s)) return rc;
     if (a.bv.on) {
         if (lds) pool_kernel<MAXD, true, true, kPix><<<grid, 64, ldsb, s>>>(a);
         else pool_kernel<MAXD, false, true, kPix><<<grid, 64, ldsb, s>>>(a);
@@ -1443,15 +1467,28 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
         else pool_kernel<MAXD, false, false, kPix><<<grid, 64, ldsb, s>>>(a);
     }
     e = hipGetLastError();
-    if (e != hipSuccess) return hip_fail(e, "pool_kernel launch");
-    if (record) LRT_HIP(hipEventRecord(users[0]->ev_rec, s));
+    if (e != hipSuccess) {
+        if (record) users[0]->state = 0;   // nothing recorded: the entry is free again
+        return hip_fail(e, "pool_kernel launch");
+    }
+    if (record) {   // the costs just recorded, sorted on the device behind the launch
+        Context::TileOrder& o = *users[0];
+        e = sort_tiles_desc(o.d_cost, o.d_keys, o.d_ids, o.d_perm, (int)ntiles, o.d_tmp, &o.tmp_bytes, s);
+        if (e == hipSuccess) e = hipEventRecord(o.ev_rec, s);
+        if (e != hipSuccess) {
+            o.state = 0;   // no order for this signature: the next launch records again
+            return hip_fail(e, "tile order sort");
+        }
+    }
     for (auto* u : users)
         if (u)
             if (int rc = order_used(*u, s)) return rc;
+    // order: 0 queue order (tile order off), 1 recording in queue order, 2 the signature's own
+    // sorted order, 3 recording with the order borrowed from the same geometry
     snprintf(g_last_launch, sizeof(g_last_launch),
              "kernel=pool_kernel maxd=%d lds=%d bvh=%d pix=%d ns=%d grid=%u tasks=%lld order=%d per_cu=%d", MAXD,
              lds ? 1 : 0, a.bv.on ? 1 : 0, kPix, fixed ? kFixedSpheres : 0, grid.x, ntiles,
-             users[0] && users[0]->state == 2 ? 2 : users[1] ? 3 : record ? 1 : 0, per_cu);
+             !users[0] ? 0 : !record ? 2 : users[1] ? 3 : 1, per_cu);
 #ifdef LRT_EXP_SECSTATS
     secstats_dump(d_sec, s);
 #endif
@@ -1837,29 +1874,52 @@ bool host_pipeline(const lrt_render_desc* d, size_t bytes) {
            d->row_count >= Context::kHostChunks;
 }
 
-int host_chunks() {   // row chunks of the DMA copy (LRT_HOST_CHUNKS, 1..8)
+// Row chunks of the DMA copy (LRT_HOST_CHUNKS, 1..8; default 4 for DrawTest's look-ahead calls,
+// whose lerps follow the copy chunk by chunk: 0.47 vs 0.50 ms at 2; 2 otherwise, where the
+// render sets the pace: 0.53 vs 0.54 ms at 4 -- profiles/r3_m, r3_o).
+int host_chunks(bool lookahead) {
     static const int k = [] {
         const char* e = getenv("LRT_HOST_CHUNKS");
-        const int v = e ? atoi(e) : 2;
-        return v < 1 ? 1 : v > Context::kHostChunks ? Context::kHostChunks : v;
+        const int v = e ? atoi(e) : 0;
+        return v < 0 ? 1 : v > Context::kHostChunks ? Context::kHostChunks : v;
     }();
-    return k;
+    return k > 0 ? k : lookahead ? 4 : 2;
 }
 
 // lrt_draw_test's look-ahead (LRT_DRAW_LOOKAHEAD, default on). DrawTest's colours depend on
 // frameCount, the size and the scene only (parallel.cpp:297-323: `time` is unused, the camera
 // is rebuilt from the size), and the reference's caller asks for frameCount + 1 next
-// (main.cpp:165,187). So after a pipelined call has enqueued its own work, the colours of the
-// next frame are rendered on the same stream; the call returns once its own work is done. A
-// later call with exactly that render (desc and scene version compared) lerps those colours
-// and skips its render, so the render leaves the call's critical path (DMA in -> lerp ->
-// PCIe out); any other call renders as before. Same kernel, same seeds: the same bits.
+// (main.cpp:165,187). So a pipelined DrawTest call also renders the colours of the next
+// frame, on a stream of their own that runs beside this call's DMA and PCIe-write lerps (a
+// hit: from the call's start; a miss: after its own render), CU-masked so that the lerps
+// still find CUs (LRT_LOOKAHEAD_RESERVED, default 32 = 4 per XCD; 0-32 within 0.01 ms pinned,
+// 32 best pageable: profiles/r3_o); the call returns once its
+// own work is done. A later call asking for exactly that render (desc and scene version
+// compared) lerps those colours and skips its render, so the render leaves the critical
+// path (DMA in -> lerp -> PCIe out); any other call renders as before. Same kernel, same
+// seeds: the same bits. Two colour buffers alternate (one read by this call's lerps, the
+// other written by the next look-ahead).
 bool draw_lookahead_on() {
     static const bool on = [] {
         const char* e = getenv("LRT_DRAW_LOOKAHEAD");
         return !(e && atoi(e) == 0);
     }();
     return on;
+}
+
+int lookahead_reserved_cus() {
+    static const int k = [] {
+        const char* e = getenv("LRT_LOOKAHEAD_RESERVED");
+        return e ? atoi(e) : 32;
+    }();
+    return k;
+}
+
+// The lerp grid: a few blocks per CU, each striding over the chunk (posted PCIe writes need
+// no more in flight; a full grid would wait for CUs behind the look-ahead render)
+unsigned merge_blocks(size_t n) {
+    const size_t want = (n + 255) / 256, cap = (size_t)4 * ctx().num_cus;
+    return (unsigned)std::max<size_t>(1, std::min(want, cap));
 }
 
 int render_host_pipelined(const lrt_render_desc* d, float* buf, float* hdev, size_t bytes, long long* out_rays,
@@ -1873,7 +1933,7 @@ int render_host_pipelined(const lrt_render_desc* d, float* buf, float* hdev, siz
         LRT_HIP(hipEventCreateWithFlags(&ctx().ev_ret, hipEventDisableTiming));
     }
     const size_t cbytes = bytes * (size_t)d->frames;
-    // a hit: the look-ahead rendered exactly this (it is ordered before this call's lerps on s)
+    // a hit: the look-ahead rendered exactly this (this call's lerps wait for its event)
     const bool hit = la.on && la.scene_version == ctx().scene_version && memcmp(&la.d, d, sizeof(*d)) == 0;
     la.on = false;
     *ahead_state = hit ? 1 : 0;
@@ -1884,7 +1944,8 @@ int render_host_pipelined(const lrt_render_desc* d, float* buf, float* hdev, siz
         if (hipMalloc(&ctx().d_col, cbytes) != hipSuccess) return fail(LRT_E_NOMEM, "hipMalloc(sample colours)");
         ctx().col_bytes = cbytes;
     }
-    const int K = host_chunks(), rows = d->row_count, xc = d->x_count;
+    const bool ahead_on = lookahead && draw_lookahead_on() && d->frames == 1 && d->frame0 < INT_MAX - 1;
+    const int K = host_chunks(ahead_on || hit), rows = d->row_count, xc = d->x_count;
     const size_t npix = (size_t)xc * rows;
     auto chunk = [&](int c, size_t& p0, size_t& n) {   // chunk c: rows [c rows / K, (c + 1) rows / K)
         const size_t r0 = (size_t)rows * c / K, r1 = (size_t)rows * (c + 1) / K;
@@ -1897,9 +1958,11 @@ int render_host_pipelined(const lrt_render_desc* d, float* buf, float* hdev, siz
         LRT_HIP(hipMemcpyAsync(ctx().d_frame + 4 * p0, buf + 4 * p0, n * 16, hipMemcpyHostToDevice, ctx().s_in));
         LRT_HIP(hipEventRecord(ctx().ev_in[c], ctx().s_in));
     }
-    float4* col = hit ? la.col : ctx().d_col;
-    unsigned long long* d_rays = hit ? la.d_rays : ctx().d_rays;
-    if (!hit) {
+    float4* col = hit ? la.col[la.cur] : ctx().d_col;
+    unsigned long long* d_rays = hit ? la.d_rays + la.cur : ctx().d_rays;
+    if (hit) {
+        LRT_HIP(hipStreamWaitEvent(s, la.ev, 0));
+    } else {
         LRT_HIP(hipMemsetAsync(d_rays, 0, sizeof(unsigned long long), s));
         int rc = render_device(d, ctx().d_frame, d_rays, nullptr, s, col);
         if (rc) {
@@ -1907,11 +1970,52 @@ int render_host_pipelined(const lrt_render_desc* d, float* buf, float* hdev, siz
             return rc;
         }
     }
+    if (ahead_on) {
+        // the next frame's colours into the buffer pair this call does not read
+        const int nx = hit ? la.cur ^ 1 : la.cur;
+        lrt_render_desc nd = *d;
+        nd.frame0 = d->frame0 + 1;
+        bool ok = true;
+        if (!la.stream) {
+            const int n = ctx().num_cus, keep = std::max(1, n - std::max(0, lookahead_reserved_cus()));
+            std::vector<uint32_t> mask((size_t)(n + 31) / 32, 0u);
+            for (int c = 0; c < keep; ++c) mask[c / 32] |= 1u << (c % 32);   // spread over XCDs (c % 8)
+            ok = hipExtStreamCreateWithCUMask(&la.stream, (uint32_t)mask.size(), mask.data()) == hipSuccess &&
+                 hipEventCreateWithFlags(&la.ev, hipEventDisableTiming) == hipSuccess &&
+                 hipEventCreateWithFlags(&la.ev_render, hipEventDisableTiming) == hipSuccess;
+            if (ok) ctx().masked_streams.emplace_back(la.stream, keep);
+        }
+        if (ok && la.bytes[nx] < cbytes) {
+            if (la.col[nx]) (void)hipFree(la.col[nx]);
+            la.col[nx] = nullptr;
+            la.bytes[nx] = 0;
+            ok = hipMalloc(&la.col[nx], cbytes) == hipSuccess;
+            if (ok) la.bytes[nx] = cbytes;
+        }
+        if (ok && !la.d_rays) ok = hipMalloc(&la.d_rays, 2 * sizeof(unsigned long long)) == hipSuccess;
+        // a miss: after this call's own render (the two would share the CUs it needs)
+        if (ok && !hit)
+            ok = hipEventRecord(la.ev_render, s) == hipSuccess && hipStreamWaitEvent(la.stream, la.ev_render, 0) == hipSuccess;
+        if (ok) ok = hipMemsetAsync(la.d_rays + nx, 0, sizeof(unsigned long long), la.stream) == hipSuccess;
+        char keep[sizeof(g_last_launch)];   // the launch string stays this call's
+        memcpy(keep, g_last_launch, sizeof(keep));
+        if (ok) ok = render_device(&nd, ctx().d_frame, la.d_rays + nx, nullptr, la.stream, la.col[nx]) == LRT_OK;
+        memcpy(g_last_launch, keep, sizeof(keep));
+        if (ok) ok = hipEventRecord(la.ev, la.stream) == hipSuccess;
+        if (ok) {
+            la.on = true;
+            la.cur = nx;
+            la.d = nd;
+            la.scene_version = ctx().scene_version;
+        } else {
+            (void)hipGetLastError();   // no look-ahead: the next call renders for itself
+        }
+    }
     for (int c = 0; c < K; ++c) {   // each chunk's lerp once its values are in, written to the host pixels
         size_t p0, n;
         chunk(c, p0, n);
         LRT_HIP(hipStreamWaitEvent(s, ctx().ev_in[c], 0));
-        merge_to_host_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(
+        merge_to_host_kernel<<<merge_blocks(n), 256, 0, s>>>(
             col + p0, reinterpret_cast<const float4*>(ctx().d_frame) + p0, reinterpret_cast<float4*>(hdev) + p0,
             ctx().d_lerp, (int)n, d->frame0, d->frames, npix);
         LRT_HIP(hipGetLastError());
@@ -1919,33 +2023,6 @@ int render_host_pipelined(const lrt_render_desc* d, float* buf, float* hdev, siz
     unsigned long long rays = 0;
     LRT_HIP(hipMemcpyAsync(&rays, d_rays, sizeof(rays), hipMemcpyDeviceToHost, s));
     LRT_HIP(hipEventRecord(ctx().ev_ret, s));
-    if (lookahead && draw_lookahead_on() && d->frames == 1 && d->frame0 < INT_MAX - 1) {
-        // the next frame's colours, behind this call's lerps (which read `col`) on s
-        lrt_render_desc nd = *d;
-        nd.frame0 = d->frame0 + 1;
-        bool ok = true;
-        if (la.bytes < cbytes) {
-            if (la.col) (void)hipFree(la.col);
-            la.col = nullptr;
-            la.bytes = 0;
-            ok = hipMalloc(&la.col, cbytes) == hipSuccess;
-            if (ok) la.bytes = cbytes;
-        }
-        if (ok && !la.d_rays) ok = hipMalloc(&la.d_rays, sizeof(unsigned long long)) == hipSuccess;
-        if (ok) ok = hipMemsetAsync(la.d_rays, 0, sizeof(unsigned long long), s) == hipSuccess;
-        // the launch string stays this call's
-        char keep[sizeof(g_last_launch)];
-        memcpy(keep, g_last_launch, sizeof(keep));
-        if (ok) ok = render_device(&nd, ctx().d_frame, la.d_rays, nullptr, s, la.col) == LRT_OK;
-        memcpy(g_last_launch, keep, sizeof(keep));
-        if (ok) {
-            la.on = true;
-            la.d = nd;
-            la.scene_version = ctx().scene_version;
-        } else {
-            (void)hipGetLastError();   // no look-ahead: the next call renders for itself
-        }
-    }
     LRT_HIP(hipEventSynchronize(ctx().ev_ret));
     if (out_rays) *out_rays = (long long)rays;
     return LRT_OK;
@@ -2292,16 +2369,19 @@ void free_context(Context& c) {
     for (auto& m : c.masked_streams) (void)hipStreamDestroy(m.first);
     if (c.d_col) (void)hipFree(c.d_col);
     for (auto& o : c.order) {
-        if (o.d_cost) (void)hipFree(o.d_cost);
-        if (o.d_perm) (void)hipFree(o.d_perm);
+        if (o.d_base) (void)hipFree(o.d_base);
         if (o.ev_rec) (void)hipEventDestroy(o.ev_rec);
         for (auto& u : o.uses) (void)hipEventDestroy(u.second);
     }
     for (int k = 0; k < Context::kHostChunks; ++k)
         if (c.ev_in[k]) (void)hipEventDestroy(c.ev_in[k]);
     if (c.ev_ret) (void)hipEventDestroy(c.ev_ret);
-    if (c.ahead.col) (void)hipFree(c.ahead.col);
+    for (int k = 0; k < 2; ++k)
+        if (c.ahead.col[k]) (void)hipFree(c.ahead.col[k]);
     if (c.ahead.d_rays) (void)hipFree(c.ahead.d_rays);
+    if (c.ahead.ev) (void)hipEventDestroy(c.ahead.ev);
+    if (c.ahead.ev_render) (void)hipEventDestroy(c.ahead.ev_render);
+    // (c.ahead.stream is one of c.masked_streams, destroyed with them)
     if (c.ev_done) (void)hipEventDestroy(c.ev_done);
     if (c.s_in) (void)hipStreamDestroy(c.s_in);
     if (c.stream) (void)hipStreamDestroy(c.stream);

@@ -40,7 +40,7 @@ print("ok")
 
 
 @pytest.mark.parametrize("env,pinned,w,h", [
-    ({}, True, 200, 117),                                # pipelined, 2 chunks (default)
+    ({}, True, 200, 117),                                # pipelined, default chunks (4 with the look-ahead)
     ({"LRT_HOST_CHUNKS": "1"}, True, 160, 90),
     ({"LRT_HOST_CHUNKS": "3"}, True, 200, 117),          # uneven chunks
     ({"LRT_HOST_CHUNKS": "8"}, True, 96, 61),

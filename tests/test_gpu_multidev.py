@@ -162,8 +162,10 @@ def _torch_render(gpu, job, stream, out):
 
 def test_pool_order_two_streams_bitwise(gpu):
     """The bench's pipelining: config 2 launched alternately on two streams, each into its own
-    buffer, across the recording launch and the switch to the heaviest-first order. Every
-    frame equals the single-stream render (the order is uploaded before any stream reads it)."""
+    buffer, across the recording launch and the switch to the heaviest-first order, with no
+    host synchronisation in between: the order is sorted on the device behind the recording
+    launch, and every later launch, on either stream, waits for that sort's event. Every frame
+    equals the single-stream render."""
     import torch
     from learnraytracing_amd import _lib as L
     w, h = 1280, 720
@@ -175,8 +177,6 @@ def test_pool_order_two_streams_bitwise(gpu):
     for k, o in enumerate(outs):
         _torch_render(gpu, job2, streams[k % 2], o)
         orders.append(L.last_launch()["order"])
-        if k == 0:
-            torch.cuda.synchronize()   # the recording launch ends: launch 1 sorts and uploads the order
     torch.cuda.synchronize()
     want, _ = oracle.orc_render(w, h, 4, 8, cam22=cam.to22())
     for k, o in enumerate(outs):

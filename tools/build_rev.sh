@@ -9,6 +9,6 @@ git -C "$root" archive "$rev" learnraytracing_amd/csrc include | tar -x -C "$tmp
 mkdir -p "$root/build_exp"
 cd "$tmp/learnraytracing_amd/csrc"
 /opt/rocm/bin/hipcc -O3 "$@" -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize --offload-arch=gfx950 -I../../include \
-  -Wall -Wno-unused-function -shared -o "$root/build_exp/liblrt_$name.so" lrt_hip.hip -L/opt/rocm/lib -lrccl -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib
+  -Wall -Wno-unused-function -shared -o "$root/build_exp/liblrt_$name.so" lrt_hip.hip $(ls lrt_sort.hip 2>/dev/null) -L/opt/rocm/lib -lrccl -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib
 rm -rf "$tmp"
 echo "built build_exp/liblrt_$name.so ($rev $*)"

@@ -7,5 +7,5 @@ name=$1; shift
 cd "$(dirname "$0")/../learnraytracing_amd/csrc"
 mkdir -p ../../build_exp
 /opt/rocm/bin/hipcc -O3 "$@" -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize --offload-arch=gfx950 -I../../include \
-  -Wall -Wno-unused-function -DLRT_ROCTX=1 -shared -o ../../build_exp/liblrt_$name.so lrt_hip.hip -L/opt/rocm/lib -lrccl -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib
+  -Wall -Wno-unused-function -DLRT_ROCTX=1 -shared -o ../../build_exp/liblrt_$name.so lrt_hip.hip $(ls lrt_sort.hip 2>/dev/null) -L/opt/rocm/lib -lrccl -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib
 echo "built build_exp/liblrt_$name.so ($*)"
