@@ -127,6 +127,32 @@ def cpu_baseline(cfg, budget_s: float, cores: int):
                       f"{rays} rays in {dt:.2f} s, {cores} {'processes' if use_ref else 'threads'}; {src}"}
 
 
+def drawtest_leg(lrt, frames: int = 200):
+    """lrt_draw_test as src/cpu/main.cpp drives DrawTest: one pageable `new float[]` backbuffer
+    (main.cpp:40) handed to every frame (main.cpp:165) at 1280x720, kMaxDepth 20, frameCount
+    counting up. The first two frames (staged, then the registration cache page-locks the
+    buffer) are untimed; the rate is rays / wall time over the next `frames` frames, the same
+    unit as cpu_reference_drawtest (the reference's DrawTest on the host cores)."""
+    import numpy as np
+
+    from learnraytracing_amd import _lib as L
+    w, h = 1280, 720
+    bb = np.zeros(w * h * 4, np.float32)
+    for f in range(2):
+        lrt.DrawTest(0.0, f, w, h, bb)
+    rays = 0
+    t0 = time.perf_counter()
+    for f in range(2, 2 + frames):
+        rays += lrt.DrawTest(0.0, f, w, h, bb)
+    dt = time.perf_counter() - t0
+    info = L.last_launch()
+    lrt.host_unregister(bb)
+    return {"value": round(rays / dt / 1e6, 1), "unit": "Mray/s", "ms_per_frame": round(dt / frames * 1e3, 4),
+            "frames": frames, "host_path": info.get("host"), "lookahead": info.get("lookahead"),
+            "what": "lrt_draw_test(0, f, 1280, 720, pageable backbuffer) per frame, host wall clock (H2D of the "
+                    "previous values, render, lerp written back over PCIe)"}
+
+
 def cpu_reference_drawtest(cores: int, budget_s: float):
     """Context beside cpu_baseline: the reference as it ships -- its own
     DrawTest (parallel.cpp:297-323) with enkiTS over `cores` workers, kMaxDepth 20 and the
@@ -411,6 +437,10 @@ def main():
             if world > 1:
                 dist.barrier()
 
+    # ---- the reference API as its own caller uses it (rank 0, N = 1): DrawTest per frame
+    drawtest = drawtest_leg(lrt) if extra and world == 1 else None
+    torch.cuda.synchronize()
+
     stats = torch.tensor([elapsed, timed_rays, alone_ms or 0.0, e2e_s or 0.0], dtype=torch.float64,
                          device=dev if backend == "nccl" else "cpu")
     if world > 1:
@@ -502,6 +532,7 @@ def main():
             "cpu_baseline": cpu,
             "cpu_baseline_1core": cpu1,
             "cpu_reference_drawtest": cpu_dt,
+            "drawtest": drawtest,
         }
         print(json.dumps(out), flush=True)
     if rstream is not None:
