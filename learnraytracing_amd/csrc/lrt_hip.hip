@@ -1729,8 +1729,8 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     return launch_split<64>(a, lds, d->x_count, d->row_count, d->frames, want_feat, s);
 }
 
-// The library's kernel policy (measured, profiles/r2_p2, r2_p9): the pool kernel (v5) given
-// at least 4 frames and two tiles per resident wave -- BVH scenes (config 4: 223 vs 303
+// The library's kernel policy (measured, profiles/r2_p2, r2_p9, r3_t): the pool kernel (v5) given
+// at least 4 frames and a tile per resident wave -- BVH scenes (config 4: 223 vs 303
 // ms, config 5), bounce budgets above 8 (config 3: 2.45 vs 2.87 ms) and, with its
 // heaviest-first tile order (tile_order), the 8-bounce default scene too (config 2: 0.254 vs
 // 0.289 ms/step, 0.297 vs 0.329 ms for a launch alone); v0 otherwise (few pixels with many
@@ -1742,7 +1742,10 @@ int auto_kernel(const KernelArgs& a, const lrt_render_desc* d, bool feat) {
     const int tx = pix >= 128 ? 16 : pix >= 32 ? 8 : pix >= 8 ? 4 : pix >= 2 ? 2 : 1, ty = pix / tx;
     const long long tiles = (long long)((d->x_count + tx - 1) / tx) * ((d->row_count + ty - 1) / ty);
     const long long slots = 16LL * ctx().num_cus;   // resident waves (4 per SIMD)
-    return tiles >= 2 * slots ? LRT_F_POOL : LRT_F_SIMPLE;
+    // at least a tile per resident wave: config 2's row shard of 2 (7,200 tiles) runs 0.1316 ms
+    // on the pool kernel against 0.1473 on v0; a shard of 4 (3,680 tiles) 0.1456 against 0.0773
+    // (profiles/r3_t)
+    return tiles >= slots ? LRT_F_POOL : LRT_F_SIMPLE;
 }
 
 int ensure_frame(size_t bytes) {

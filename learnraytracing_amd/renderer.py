@@ -65,10 +65,13 @@ def host_unregister(backbuffer: np.ndarray) -> None:
 def DrawTest(time: float, frameCount: int, screenWidth: int, screenHeight: int,
              backbuffer: np.ndarray) -> int:
     _check_host_buffer(backbuffer, screenWidth * screenHeight * 4)
+    ptr = backbuffer.ctypes.data
     rays = ctypes.c_int(0)
     L.check(L.lib().lrt_draw_test(float(time), int(frameCount), int(screenWidth), int(screenHeight),
-                                  backbuffer.ctypes.data_as(ctypes.c_void_p), ctypes.byref(rays)))
-    if L.last_launch().get("host", "").startswith("registered"):
+                                  ctypes.c_void_p(ptr), ctypes.byref(rays)))
+    # (the launch string is parsed only until the buffer's registration is tracked: per-frame
+    # Python work delays the next call's DMA)
+    if ptr not in _registered and L.last_launch().get("host", "").startswith("registered"):
         _unregister_when_freed(backbuffer)
     return rays.value
 
