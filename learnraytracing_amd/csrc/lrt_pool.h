@@ -43,6 +43,23 @@ struct PoolTile {   // tile shape: kPix pixels, as square as a power of two allo
     static_assert(X * Y == kPix && kPix <= 256, "kPix: a power of two up to 256");
 };
 
+// The kernel arguments a path start needs (camera, window), read where they are used through
+// a pointer the compiler cannot hoist out of the loop (an empty asm launders it): held in
+// SGPRs for the whole kernel, they pushed the traversal's own state into spills.
+// (The kernel's only argument is the KernelArgs, at offset 0 of the kernarg segment; taking
+// &a instead would copy the struct to scratch.)
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef const __attribute__((address_space(4))) KernelArgs* KArgPtr;
+__device__ __forceinline__ KArgPtr opaque_args() {
+    KArgPtr p = (KArgPtr)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return p;
+}
+#else   // (the host pass only parses the kernel)
+typedef const KernelArgs* KArgPtr;
+__device__ __forceinline__ KArgPtr opaque_args() { return nullptr; }
+#endif
+
 template <int MAXD, bool kLds, bool kBvh, int kPix, int kNS = 0>
 __global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const KernelArgs a) {
     static_assert(kNS == 0 || (kLds && !kBvh), "a fixed sphere count is for the LDS linear scan");
@@ -175,14 +192,17 @@ __global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const Ker
                         if (k < N) {
                             const int j = k % kPix, f = fr0 + k / kPix;
                             const int lx = tx0 + j % TX, ly = ty0 + j / TX;
-                            if (lx < a.xc && ly < a.rows) {   // TraceRowJob's per-pixel body (:270-279)
+                            const KArgPtr pa = opaque_args();   // window and camera, read here
+                            if (lx < pa->xc && ly < pa->rows) {   // TraceRowJob's per-pixel body (:270-279)
                                 sec_count(sc, kSecCamera);
-                                const int x = a.x0 + lx;
-                                const int y = a.y0 + (ly / a.rb) * a.rb * a.rp + a.rph * a.rb + ly % a.rb;
+                                const int x = pa->x0 + lx;
+                                const int rb = pa->rb;
+                                const int y = pa->y0 + (ly / rb) * rb * pa->rp + pa->rph * rb + ly % rb;
                                 rng = PixelSeed((uint32_t)x, (uint32_t)y, (uint32_t)f);
                                 const float u = ((float)x + RandomFloat01(rng)) * invWidth;    // :272
                                 const float v = ((float)y + RandomFloat01(rng)) * invHeight;   // :273
-                                r = GetRay(a.cam, u, v, rng, sc.rnlut);
+                                const CameraDev cam = pa->cam;
+                                r = GetRay(cam, u, v, rng, sc.rnlut);
                                 depth = 0;
                                 prevLambert = false;
                                 pend = false;
@@ -283,25 +303,34 @@ __global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const Ker
             sec_enter(sc, kSecOther, false);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            const KArgPtr pa = opaque_args();   // output window, lerp table, frame: read here
+            const int xc = pa->xc, rows = pa->rows;
+            float4* const out = pa->out;
+            const float* const lerp = pa->lerp;
+            float4* const frame = pa->frame;
 #pragma unroll
             for (int j0 = 0; j0 < kPix; j0 += 64) {   // tiles above 64 pixels: several per lane
                 const int j = j0 + lane;
                 const int mx = tx0 + j % TX, my = ty0 + (j / TX) % TY;
-                if (j < kPix && mx < a.xc && my < a.rows) {
-                    float4* const mpx = a.out + (size_t)my * a.xc + mx;
+                if (j < kPix && mx < xc && my < rows) {
+                    float4* const mpx = out + (size_t)my * xc + mx;
                     float4 acc = *mpx;
                     F3 c3 = f3(acc.x, acc.y, acc.z);
                     for (int t = 0; t < nfr; ++t) {
                         const float4 c = slots[t * kPix + j];
                         const int f = fr0 + t;
-                        const float lerpFac = f < kLerpTable ? a.lerp[f] : (float)f / (float)(f + 1);
+                        const float lerpFac = f < kLerpTable ? lerp[f] : (float)f / (float)(f + 1);
                         c3 = c3 * lerpFac + f3(c.x, c.y, c.z) * (1.0f - lerpFac);
                     }
                     acc.x = c3.x;
                     acc.y = c3.y;
                     acc.z = c3.z;
                     *mpx = acc;   // alpha as read
-                    if (a.frame) a.frame[(size_t)GlobalRow(a, my) * a.width + a.x0 + mx] = acc;   // the exchange, fused
+                    if (frame) {   // the exchange, fused: the pixel at its global row (GlobalRow)
+                        const int rb = pa->rb;
+                        const int gy = pa->y0 + (my / rb) * rb * pa->rp + pa->rph * rb + my % rb;
+                        frame[(size_t)gy * pa->width + pa->x0 + mx] = acc;
+                    }
                 }
             }
             // the next round overwrites the slots: every read above completes first
