@@ -56,6 +56,10 @@ BYTES_PER_PIXEL_SAMPLE = 24.0    # 12 B read + 12 B write of RGB 
 # (the 157.3 TFLOP/s FP32 vector peak of MI355X_MICROARCH.md counts an FMA as 2)
 VALU_LANE_PEAK_T = 256 * 4 * 32 * 2.4e9 / 1e12
 VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2   # wave64 VALU instructions/s (2 cycles each per SIMD)
+FP32_PEAK_T = 157.3              # MI355X_MICROARCH.md: peak FP32 (vector), TFLOP/s
+# algorithmic FLOPs per counted ray = 17 per sphere test (HitSphere, maths.cpp:54-59,
+# one per sphere of the linear scan) + ~60 of shading = 213 for the reference's 9-sphere scene
+ALG_FLOP_PER_SPHERE, ALG_FLOP_SHADING = 17, 60
 PMC_INDEX = os.path.join(ROOT, "profiles", "pmc_index.json")
 
 
@@ -471,10 +475,11 @@ def main():
                        "duration alone (ms_per_launch_alone); traffic = corrected 2 x FETCH_SIZE + WRITE_SIZE "
                        "per launch from the committed PMC pass"}
         roof = hbm
+        valu = None
         if pmc and "lane_ops_per_launch" in pmc:
             lane_ops = pmc["lane_ops_per_launch"]
             achieved_t = lane_ops / (dur_ms * 1e-3) / 1e12
-            roof = {"bound": "valu", "achieved": round(achieved_t, 3), "peak": round(VALU_LANE_PEAK_T, 2),
+            valu = {"bound": "valu", "achieved": round(achieved_t, 3), "peak": round(VALU_LANE_PEAK_T, 2),
                     "unit": "TFLOP/s", "frac": round(achieved_t / VALU_LANE_PEAK_T, 4),
                     "traffic": hbm["traffic"], "kernel": kname,
                     "lane_ops_per_launch": lane_ops,
@@ -482,11 +487,32 @@ def main():
                     "lane_util": pmc["lane_util"],
                     "duration_ms": round(dur_ms, 4),
                     "source": pmc["path"],
-                    "note": "FP32 VALU lane-operations/s: SQ_INSTS_VALU x 64 x lane_util per launch "
-                            "(lane_util = SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU x 64), committed PMC "
-                            "pass) over one launch's duration alone, measured here with HIP events; peak = "
-                            "256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T lane-ops/s (the 157.3 TFLOP/s "
-                            "FP32 vector peak counts an FMA as 2); frac = issue_frac x lane_util"}
+                    "note": "ISSUED work, not algorithmic: FP32 VALU lane-operations/s = SQ_INSTS_VALU x 64 x "
+                            "lane_util per launch (lane_util = SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU x 64), "
+                            "committed PMC pass) over one launch's duration alone; peak = 256 CU x 4 SIMD x 32 "
+                            "lanes x 2.4 GHz = 78.6 T lane-ops/s; frac = issue_frac x lane_util"}
+        if cfg["scene"] == "default":
+            # the algorithmic roofline of the prompt: SURVEY §8(d)'s FLOPs per counted ray x the rays
+            # one launch counts (rank 0's launch) / that launch's duration alone, against the FP32
+            # vector peak. (For the 1000-sphere scene §8(d)'s 17 N per ray is the linear scan's
+            # work, which the BVH does not do; there the counter line above is the roofline.)
+            nsph = 9
+            flop_ray = ALG_FLOP_PER_SPHERE * nsph + ALG_FLOP_SHADING
+            rays_launch = rays_per_step / max(1, world)
+            alg_t = flop_ray * rays_launch / (dur_ms * 1e-3) / 1e12
+            roof = {"bound": "valu", "achieved": round(alg_t, 3), "peak": FP32_PEAK_T, "unit": "TFLOP/s",
+                    "frac": round(alg_t / FP32_PEAK_T, 4),
+                    "traffic": hbm["traffic"], "kernel": kname,
+                    "algorithmic_flop_per_ray": flop_ray,
+                    "rays_per_launch": int(rays_launch),
+                    "duration_ms": round(dur_ms, 4),
+                    "note": f"ALGORITHMIC: SURVEY 8(d) {flop_ray} FLOP per counted ray (17 per sphere x {nsph} + 60 "
+                            "shading) x the launch's counted rays over one launch's duration alone (HIP events on "
+                            "its stream); peak = MI355X FP32 vector peak 157.3 TFLOP/s, which counts an FMA as 2 "
+                            "(the bit-exact path is built with -ffp-contract=off, so its own ceiling is half that); "
+                            "traffic = corrected HBM bytes per launch from the committed PMC pass"}
+        elif valu:
+            roof = valu
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -520,6 +546,7 @@ def main():
                 "instance": " ".join(f"{k}={v}" for k, v in launch_info.items() if k != "kernel"),
             },
             "roofline": roof,
+            "roofline_valu_issue": valu if valu is not roof else None,
             "roofline_hbm": hbm,
             "end_to_end": {
                 "value": round(total_rays / args.steps * e2e_steps / e2e_s / 1e6, 3), "unit": "Mray/s",
