@@ -271,7 +271,7 @@ def main():
             dist.init_process_group(backend)
     import learnraytracing_amd as lrt
     from learnraytracing_amd import _lib as L
-    from learnraytracing_amd.dist import SharedFrames, gather_to_root, max_shard_rows, shard_rows
+    from learnraytracing_amd.dist import gather_to_root, max_shard_rows, open_shared_frames, shard_rows
     from learnraytracing_amd.renderer import pack_rgb_tensor, render_tensor_to_frame, unshard_rgb_tensor
 
     lrt.InitializeTest()
@@ -303,7 +303,13 @@ def main():
     # remote exchange: rank 0's frames mapped into every rank; each render stores its finished
     # pixels there itself (no pack, gather or unshard launch per step)
     remote = world > 1 and args.exchange == "remote"
-    shared = SharedFrames(W, H, nslots, rank) if remote else None
+    shared = None
+    if remote:
+        dev_b = dev if backend == "nccl" else torch.device("cpu")
+        shared = open_shared_frames(W, H, nslots, rank, dev_b)
+        if shared is None:   # IPC mapping refused on some rank: the RCCL exchange instead
+            log("note: IPC frame mapping failed on a rank; falling back to --exchange rccl")
+            remote = False
     gather_ex = world > 1 and not remote
     # the RCCL exchange carries RGB only (lrt_pack_rgb): 12 of the 16 bytes per pixel cross xGMI
     packed = [torch.empty((max_rows, W, 3), dtype=torch.float32, device=dev) if gather_ex else None

@@ -92,24 +92,37 @@ class SharedFrames:
         self.bytes = width * height * 16
         self._owned, self._opened, self.ptrs = [], [], []
         handles = None
+        err = None
         if rank == 0:
             handles = []
-            for _ in range(count):
-                p = ctypes.c_void_p()
-                h = (ctypes.c_char * L.IPC_HANDLE_BYTES)()
-                L.check(L.lib().lrt_ipc_alloc(self.bytes, ctypes.byref(p), ctypes.cast(h, ctypes.c_void_p)))
-                self._owned.append(p.value)
-                handles.append(bytes(h))
+            try:
+                for _ in range(count):
+                    p = ctypes.c_void_p()
+                    h = (ctypes.c_char * L.IPC_HANDLE_BYTES)()
+                    L.check(L.lib().lrt_ipc_alloc(self.bytes, ctypes.byref(p), ctypes.cast(h, ctypes.c_void_p)))
+                    self._owned.append(p.value)
+                    handles.append(bytes(h))
+            except Exception as e:   # still broadcast (None), so no rank waits on a dead root
+                err, handles = e, None
             self.ptrs = list(self._owned)
         box = [handles]
         if dist.is_initialized():
             dist.broadcast_object_list(box, src=0, group=group)
+        if err is not None:
+            self.close()
+            raise err
+        if box[0] is None:
+            raise RuntimeError("rank 0 could not allocate the shared frames")
         if rank != 0:
-            for hb in box[0]:
-                h = (ctypes.c_char * L.IPC_HANDLE_BYTES).from_buffer_copy(hb)
-                p = ctypes.c_void_p()
-                L.check(L.lib().lrt_ipc_open(ctypes.cast(h, ctypes.c_void_p), ctypes.byref(p)))
-                self._opened.append(p.value)
+            try:
+                for hb in box[0]:
+                    h = (ctypes.c_char * L.IPC_HANDLE_BYTES).from_buffer_copy(hb)
+                    p = ctypes.c_void_p()
+                    L.check(L.lib().lrt_ipc_open(ctypes.cast(h, ctypes.c_void_p), ctypes.byref(p)))
+                    self._opened.append(p.value)
+            except Exception:
+                self.close()
+                raise
             self.ptrs = list(self._opened)
 
     def tensor(self, i: int):
@@ -135,6 +148,31 @@ class _CudaArray:
     def __init__(self, ptr: int, shape):
         self.__cuda_array_interface__ = {"shape": tuple(shape), "typestr": "<f4", "data": (int(ptr), False),
                                          "version": 3, "strides": None}
+
+
+def open_shared_frames(width: int, height: int, count: int, rank: int, device, group=None):
+    """SharedFrames on every rank, or None on every rank when any rank fails to allocate or
+    map them (the ranks agree through one all-reduce), so the caller can fall back to the
+    RCCL exchange instead of one rank dying while the others wait in a collective."""
+    import torch
+    import torch.distributed as dist
+
+    frames, err = None, None
+    try:
+        frames = SharedFrames(width, height, count, rank, group=group)
+    except Exception as e:
+        err = e
+    if not dist.is_initialized():
+        if err is not None:
+            raise err
+        return frames
+    bad = torch.tensor([0 if err is None else 1], dtype=torch.int32, device=device)
+    dist.all_reduce(bad, op=dist.ReduceOp.MAX, group=group)
+    if int(bad.item()):
+        if frames is not None:
+            frames.close()
+        return None
+    return frames
 
 
 def _tensor_from_ptr(ptr: int, shape):

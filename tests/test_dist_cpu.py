@@ -65,3 +65,45 @@ def test_two_rank_gloo_assembly_bitwise(tmp_path, world, rb):
     got = np.load(tmp_path / "frame.npy")
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
     assert int(np.load(tmp_path / "rays.npy")[0]) == wrays
+
+
+def _shared_worker(rank, world, port, fail_rank, outdir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root]
+    import torch
+    import torch.distributed as dist
+    from learnraytracing_amd import dist as D
+
+    closed = []
+
+    class Fake:   # stands in for the IPC-mapped frames: fails on fail_rank only
+        def __init__(self, w, h, n, r, group=None):
+            if r == fail_rank:
+                raise RuntimeError("hipIpcOpenMemHandle refused (test)")
+
+        def close(self):
+            closed.append(rank)
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        D.SharedFrames = Fake
+        got = D.open_shared_frames(8, 4, 2, rank, torch.device("cpu"))
+        np.save(os.path.join(outdir, f"r{rank}.npy"),
+                np.array([got is None, rank in closed], dtype=np.int32))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_rank", [-1, 0, 1])
+def test_shared_frames_failure_is_agreed(tmp_path, fail_rank):
+    """bench.py's fused exchange falls back to the RCCL gather when any rank cannot map rank
+    0's frames: every rank gets None together (no rank left waiting in a collective), and
+    the ranks that did map them close them again."""
+    world = 2
+    mp.spawn(_shared_worker, args=(world, _free_port(), fail_rank, str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        is_none, closed = np.load(tmp_path / f"r{r}.npy")
+        assert bool(is_none) == (fail_rank >= 0)
+        assert bool(closed) == (fail_rank >= 0 and r != fail_rank)
