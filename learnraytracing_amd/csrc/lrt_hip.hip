@@ -1303,7 +1303,17 @@ int order_used(Context::TileOrder& e, hipStream_t s) {
 // Picks a's order for this launch: a.perm (null: queue order) and, for the recording launch,
 // a.tcost. *users gets the entries whose buffers the launch touches (order_used after it).
 hipError_t sort_tiles_desc(const unsigned* cost_in, unsigned* keys_out, const int* ids_in, int* perm_out, int n,
-                           void* tmp, size_t* tmp_bytes, hipStream_t s);   // lrt_sort.hip
+                           void* tmp, size_t* tmp_bytes, hipStream_t s, unsigned end_bit = 32);   // lrt_sort.hip
+// LRT_POOL_PROBE: 0 off; 1 (default) a new signature without an order of the same geometry
+// to borrow probes its tiles (probe_kernel) and runs its recording launch in the probe's
+// order; 2 probes even when it could borrow
+int pool_probe_mode() {
+    static const int m = [] {
+        const char* e = getenv("LRT_POOL_PROBE");
+        return e ? atoi(e) : 1;
+    }();
+    return m;
+}
 hipError_t fill_iota(int* v, int n, hipStream_t s);
 
 // Sizes entry e for ntiles tiles (at least 65,536, so views of other sizes rarely reallocate).
@@ -1457,6 +1467,29 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     bool record = false;
     Context::TileOrder* users[2];
     if (int rc = tile_order(a, kPix, ntiles, record, users, s)) return rc;
+    bool probed = false;
+    if (record && pool_probe_mode() > 0 && (pool_probe_mode() == 2 || !users[1])) {
+        // no measured order to go by: probe the tiles' costs, sort them, and let this
+        // (recording) launch take its tiles in that order (probe_kernel, lrt_pool.h)
+        Context::TileOrder& o = *users[0];
+        KernelArgs pa = a;
+        pa.bvh_stack_offset = 0;
+        const unsigned pblocks = (unsigned)((ntiles + 64 / kProbe - 1) / (64 / kProbe));
+        if (a.bv.on) probe_kernel<true><<<pblocks, 64, bstk, s>>>(pa, o.d_cost, (int)ntiles, TX, TY);
+        else probe_kernel<false><<<pblocks, 64, 0, s>>>(pa, o.d_cost, (int)ntiles, TX, TY);
+        e = hipGetLastError();
+        if (e == hipSuccess) {
+            probe_order_kernel<<<1, 1024, 0, s>>>(o.d_cost, o.d_perm, (int)ntiles);
+            e = hipGetLastError();
+        }
+        if (e != hipSuccess) {
+            o.state = 0;
+            return hip_fail(e, "tile cost probe");
+        }
+        a.perm = o.d_perm;
+        users[1] = nullptr;   // (a borrowed order, if any, is not used)
+        probed = true;
+    }
     if (a.bv.on) {
         if (lds) pool_kernel<MAXD, true, true, kPix><<<grid, 64, ldsb, s>>>(a);
         else pool_kernel<MAXD, false, true, kPix><<<grid, 64, ldsb, s>>>(a);
@@ -1484,11 +1517,12 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
         if (u)
             if (int rc = order_used(*u, s)) return rc;
     // order: 0 queue order (tile order off), 1 recording in queue order, 2 the signature's own
-    // sorted order, 3 recording with the order borrowed from the same geometry
+    // sorted order, 3 recording with the order borrowed from the same geometry, 4 recording in
+    // the probe's order
     snprintf(g_last_launch, sizeof(g_last_launch),
              "kernel=pool_kernel maxd=%d lds=%d bvh=%d pix=%d ns=%d grid=%u tasks=%lld order=%d per_cu=%d", MAXD,
              lds ? 1 : 0, a.bv.on ? 1 : 0, kPix, fixed ? kFixedSpheres : 0, grid.x, ntiles,
-             !users[0] ? 0 : !record ? 2 : users[1] ? 3 : 1, per_cu);
+             !users[0] ? 0 : !record ? 2 : probed ? 4 : users[1] ? 3 : 1, per_cu);
 #ifdef LRT_EXP_SECSTATS
     secstats_dump(d_sec, s);
 #endif

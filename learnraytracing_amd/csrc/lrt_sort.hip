@@ -18,9 +18,9 @@ __global__ void iota_kernel(int* v, int n) {
 // tmp == nullptr: *tmp_bytes = the scratch the sort needs for n keys. Otherwise enqueues on s:
 // perm_out = tile ids ordered by cost_in descending (stable), keys_out = the sorted costs.
 hipError_t sort_tiles_desc(const unsigned* cost_in, unsigned* keys_out, const int* ids_in, int* perm_out, int n,
-                           void* tmp, size_t* tmp_bytes, hipStream_t s) {
+                           void* tmp, size_t* tmp_bytes, hipStream_t s, unsigned end_bit) {
     return rocprim::radix_sort_pairs_desc(tmp, *tmp_bytes, cost_in, keys_out, ids_in, perm_out, (unsigned)n, 0u,
-                                          32u, s);
+                                          end_bit, s);
 }
 
 hipError_t fill_iota(int* v, int n, hipStream_t s) {
