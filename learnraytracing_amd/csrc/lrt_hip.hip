@@ -1540,19 +1540,31 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
 
 // Pixels per pool tile: a round holds kPoolSamples samples, so more frames -> fewer pixels.
 // Bigger tiles make bigger pools (a round's tail, its last paths with most lanes idle, is a
-// smaller share) but fewer tiles per wave (the launch's tail).
-int pool_pixels(int frames) {
+// smaller share) but fewer tiles per wave (the launch's tail). 64 px at most by default:
+// 128-px tiles (LRT_POOL_PIX_MAX=128; taken only while every resident wave still gets one)
+// run config 2 pipelined over two streams at 0.2357/0.2373 ms/step against 0.2465/0.2476 and
+// config 3 at 1.942/1.936 against 1.950/1.953, but a launch alone at 0.363-0.412 ms against
+// 0.286-0.300 (config 3: 2.47-2.66 ms against 2.07-2.09): the few heavy 128-px tiles set the
+// end of a launch that no other launch overlaps (profiles/r3_ag, r3_fin2). 256 px left waves
+// idle on config 2 (39.4 vs 46.3 Grays/s, r3_g).
+int pool_tiles(int pix, int xc, int rows) {
+    const int tx = pix >= 128 ? 16 : pix >= 32 ? 8 : pix >= 8 ? 4 : pix >= 2 ? 2 : 1, ty = pix / tx;
+    return ((xc + tx - 1) / tx) * ((rows + ty - 1) / ty);
+}
+int pool_pixels(int frames, int xc, int rows) {
     static const int cap = [] {   // LRT_POOL_PIX_MAX: largest tile (A/B)
         const char* e = getenv("LRT_POOL_PIX_MAX");
         return e ? atoi(e) : 64;
     }();
+    const long long slots = 16LL * ctx().num_cus;   // resident waves (4 per SIMD)
     for (int pix : {256, 128, 64, 32, 16})
-        if (cap >= pix && pix * frames <= kPoolSamples) return pix;
+        if (cap >= pix && pix * frames <= kPoolSamples && (pix <= 64 || pool_tiles(pix, xc, rows) >= slots))
+            return pix;
     return 4 * frames <= kPoolSamples ? 4 : 1;
 }
 template <int MAXD>
 int launch_pool_split(const KernelArgs& a, bool lds, int xc, int rows, int frames, hipStream_t s) {
-    switch (pool_pixels(frames)) {
+    switch (pool_pixels(frames, xc, rows)) {
         case 256: return launch_pool<MAXD, 256>(a, lds, xc, rows, s);
         case 128: return launch_pool<MAXD, 128>(a, lds, xc, rows, s);
         case 64: return launch_pool<MAXD, 64>(a, lds, xc, rows, s);
@@ -1772,9 +1784,8 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
 int auto_kernel(const KernelArgs& a, const lrt_render_desc* d, bool feat) {
     if (feat || d->frames < 4) return LRT_F_SIMPLE;
     if (!(a.bv.on || d->max_depth > 8) && !pool_order_on()) return LRT_F_SIMPLE;
-    const int pix = pool_pixels(d->frames);
-    const int tx = pix >= 128 ? 16 : pix >= 32 ? 8 : pix >= 8 ? 4 : pix >= 2 ? 2 : 1, ty = pix / tx;
-    const long long tiles = (long long)((d->x_count + tx - 1) / tx) * ((d->row_count + ty - 1) / ty);
+    const int pix = pool_pixels(d->frames, d->x_count, d->row_count);
+    const long long tiles = pool_tiles(pix, d->x_count, d->row_count);
     const long long slots = 16LL * ctx().num_cus;   // resident waves (4 per SIMD)
     // at least a tile per resident wave: config 2's row shard of 2 (7,200 tiles) runs 0.1316 ms
     // on the pool kernel against 0.1473 on v0; a shard of 4 (3,680 tiles) 0.1456 against 0.0773

@@ -55,11 +55,20 @@ def main():
     os.makedirs(out, exist_ok=True)
     summary = {"kernel": KERNEL, "config": c, "key": key,
                "recipe": f"tools/gpu.sh trace={c} pmc={c},fetch pmc={c},write pmc={c},sq"}
+    # the render kernel the traced bench line names (its DrawTest leg runs trace_kernel too,
+    # and at config 2 that leg takes longer than the measured launches)
+    for f in glob.glob(os.path.join(prof, f"trace_c{c}_*.log")):
+        for line in open(f):
+            if line.startswith("{"):
+                try:
+                    KERNEL = json.loads(line)["config"]["kernel"]
+                except (ValueError, KeyError):
+                    pass
     for f in glob.glob(os.path.join(prof, "**", f"trace_c{c}_kernel_stats.csv"), recursive=True):
         rows = [r for r in csv.DictReader(open(f)) if is_render(r["Name"])]
-        if rows:   # the render kernel of this run: the one with the most time
+        if rows and not KERNEL:   # else the render kernel with the most time
             KERNEL = max(rows, key=lambda r: float(r["Percentage"]))["Name"].split("<")[0].split("::")[-1]
-            summary["kernel"] = KERNEL
+        summary["kernel"] = KERNEL
         for r in rows:
             if KERNEL in r["Name"]:
                 summary["kernel_trace"] = {"name": r["Name"], "calls": int(r["Calls"]),
