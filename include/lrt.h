@@ -285,7 +285,8 @@ int lrt_present_bgra8(const float* d_rgba, uint32_t* d_bgra, int width, int heig
 
 /* ---- diagnostics (libm restatement, lrt_libm.h) --------------------------- */
 /* kind 0: sinf, 1: cosf, 2: powf(x, 5), 3: powf(x, 0.416666667f) (LinearToSRGB),
- * 4: sqrtf, 5: 1.0f / x (the device evaluates the path's short correctly rounded sequences).
+ * 4: sqrtf, 5: 1.0f / x (the device evaluates the path's short correctly rounded sequences),
+ * 6 / 7: the sine / cosine results of the path's sincosf (one shared reduction).
  * Host evaluation of the restatement. */
 int lrt_libm_eval_host(int kind, const float* in, float* out, long long n);
 /* Device evaluation of the same restatement (device pointers, blocking). */

@@ -496,6 +496,11 @@ __global__ void present_kernel(const float4* __restrict__ src, uint32_t* __restr
 }
 
 LRT_HD float libm_eval(int kind, float x) {
+    if (kind == 6 || kind == 7) {   // the path's sincosf (one reduction, both results)
+        float sn, cs;
+        libm::sincosf(x, &sn, &cs);
+        return kind == 6 ? sn : cs;
+    }
     return kind == 0   ? libm::sinf(x)
            : kind == 1 ? libm::cosf(x)
            : kind == 2 ? libm::powf5(x)
@@ -3047,14 +3052,14 @@ int lrt_bvh_eval(const lrt_sphere* spheres, int count, const float* rays, int n,
 }
 
 int lrt_libm_eval_host(int kind, const float* in, float* out, long long n) {
-    if (kind < 0 || kind > 5 || !in || !out || n < 0) return fail(LRT_E_INVALID, "invalid libm eval arguments");
+    if (kind < 0 || kind > 7 || !in || !out || n < 0) return fail(LRT_E_INVALID, "invalid libm eval arguments");
     for (long long i = 0; i < n; ++i)
         out[i] = libm_eval(kind, in[i]);
     return LRT_OK;
 }
 
 int lrt_libm_eval_device(int kind, const float* d_in, float* d_out, long long n) {
-    if (kind < 0 || kind > 5 || !d_in || !d_out || n < 0) return fail(LRT_E_INVALID, "invalid libm eval arguments");
+    if (kind < 0 || kind > 7 || !d_in || !d_out || n < 0) return fail(LRT_E_INVALID, "invalid libm eval arguments");
     if (n == 0) return LRT_OK;
     libm_kernel<<<(unsigned)((n + 255) / 256), 256, 0, nullptr>>>(kind, d_in, d_out, n);
     LRT_HIP(hipGetLastError());

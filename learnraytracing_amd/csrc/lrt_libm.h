@@ -121,29 +121,36 @@ LRT_HD float cosf(float y) {
     return sinf_poly(x * s, x * x, sincos_poly((n & 2) ? 1 : 0), n ^ 1);
 }
 
-// sinf and cosf of the same argument with one shared reduction (glibc's sincosf
-// computes both exactly like this, and each result has the bits of the single call).
+// sinf and cosf of the same argument with one shared reduction (glibc's sincosf computes
+// both like this, and each result has the bits of the single call), in a branch-free form
+// with the same double operations, so each result has the same bits:
+//  * |y| < 0.75 (abstop12 below pi/4's: glibc's direct branch, table 0, n = 0) needs no
+//    branch of its own: there reduce_fast gives n = 0 (|y| 2/pi 2^24 < 2^23) and
+//    fma(-0, pi/2, x) = x, s = 1, table 0 -- the general path's very operations;
+//  * table 1 is table 0 with the cosine coefficients negated and the sine ones equal, and
+//    round-to-nearest is symmetric (fma(-a, b, -c) = -fma(a, b, c), (float)-d = -(float)d),
+//    so its cosine polynomial is exactly the negated table-0 one: one evaluation, a sign;
+//  * the sine and cosine polynomials are each evaluated once and swapped for odd n (glibc's
+//    sinf_poly picks by n & 1), instead of both per output.
+// Checked against glibc over the path's whole domain and beyond (tests/test_libm.py, kinds 6
+// and 7) and on the device (tests/test_gpu_parity.py).
 LRT_HD void sincosf(float y, float* sinp, float* cosp) {
-    double x = y;
-    if (abstop12(y) < abstop12(0x1.921FB6p-1f)) {
-        if (abstop12(y) < abstop12(0x1p-12f)) {
-            *sinp = y;
-            *cosp = 1.0f;
-            return;
-        }
-        const SinCosPoly p = sincos_poly(0);
-        const double x2 = x * x;
-        *sinp = sinf_poly(x, x2, p, 0);
-        *cosp = sinf_poly(x, x2, p, 1);
-        return;
-    }
     int n;
-    x = reduce_fast(x, &n);
+    const double x = reduce_fast((double)y, &n);
     const double s = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;
-    const SinCosPoly p = sincos_poly((n & 2) ? 1 : 0);
+    const SinCosPoly p = sincos_poly(0);
     const double xs = x * s, x2 = x * x;
-    *sinp = sinf_poly(xs, x2, p, n);
-    *cosp = sinf_poly(xs, x2, p, n ^ 1);
+    const float S = sinf_poly(xs, x2, p, 0);   // odd polynomial (sin coefficients: both tables)
+    float C = sinf_poly(xs, x2, p, 1);         // even polynomial, table 0
+    if (n & 2) C = -C;                         // table 1
+    const bool odd = (n & 1) != 0;
+    float sn = odd ? C : S, cs = odd ? S : C;
+    if (abstop12(y) < abstop12(0x1p-12f)) {    // glibc's tiny-argument results
+        sn = y;
+        cs = 1.0f;
+    }
+    *sinp = sn;
+    *cosp = cs;
 }
 
 // ---- powf: powf_log2_data.c (POWF_LOG2_TABLE_BITS 4, POWF_SCALE_BITS 0) ----

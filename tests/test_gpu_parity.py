@@ -245,6 +245,9 @@ def test_libm_device_exhaustive_path_domain(gpu, manifest):
     lm = manifest["libm"]
     assert hashlib.sha256(dev(0, phi).tobytes()).hexdigest() == lm["sinf_sha256"]
     assert hashlib.sha256(dev(1, phi).tobytes()).hexdigest() == lm["cosf_sha256"]
+    # the path's branch-free sincosf (lrt_libm.h): both results over the same domain
+    assert hashlib.sha256(dev(6, phi).tobytes()).hexdigest() == lm["sinf_sha256"]
+    assert hashlib.sha256(dev(7, phi).tobytes()).hexdigest() == lm["cosf_sha256"]
     pw = torch.from_numpy(np.linspace(0, 1, 1 << 20, dtype=np.float32)).cuda()
     assert hashlib.sha256(dev(2, pw).tobytes()).hexdigest() == lm["powf5_linspace01_2p20_sha256"]
     sr = torch.from_numpy(np.linspace(0, 64, 1 << 20, dtype=np.float32)).cuda()
