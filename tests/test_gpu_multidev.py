@@ -288,3 +288,18 @@ def test_drawtest_lookahead_hits_and_misses(gpu):
         run([(11, "miss"), (12, "hit")], w2, h2, bb2, want2, spheres=s, mats=m)
     finally:
         gpu.set_scene(*gpu.default_scene())
+
+
+def test_probe_order_many_tiles_equals_v0(gpu):
+    """The probe's counting sort over more tiles than one pass of its workgroup holds
+    (1920x704 at 64 px: 21,120 tiles > 16,384): the probe-ordered first launch renders every
+    tile exactly once -- its pixels and ray count equal v0's render of the same frame."""
+    from learnraytracing_amd import _lib as L
+    kw = dict(width=1920, height=704, frames=4, max_depth=8)
+    buf, rays = _host(gpu, gpu.Job(flags=512, **kw))
+    info = L.last_launch()
+    assert info["kernel"] == "pool_kernel" and info["order"] == "4" and int(info["tasks"]) > 16384, info
+    want, wrays = _host(gpu, gpu.Job(flags=2, **kw))
+    assert L.last_launch()["kernel"] == "trace_kernel"
+    _bitwise(buf, want, "probe order over 21,120 tiles vs v0")
+    assert rays == wrays
