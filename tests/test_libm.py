@@ -4,7 +4,7 @@ calls), bit for bit. The device build is checked in tests/test_gpu_parity.py.
 
 Default runs cover the path's whole sin/cos domain (2^24 inputs) and a dense sample
 of the powf domains; LRT_EXHAUSTIVE=1 sweeps every float of [0, 1] for powf(x, 5)
-and of +/-[0, 120) for sinf/cosf (minutes)."""
+and of +/-[0, 120) for sinf/cosf and the path's sincosf (minutes)."""
 import ctypes
 import hashlib
 import os
@@ -96,8 +96,8 @@ def test_exhaustive_sweeps():
         u = np.arange(lo, min(lo + step, int(top)), dtype=np.uint32)
         for sgn in (0, 0x80000000):
             x = (u | np.uint32(sgn)).view(np.float32)
-            assert_same(0, x)
-            assert_same(1, x)
+            for kind in (0, 1, 6, 7):   # sinf, cosf, and both results of sincosf
+                assert_same(kind, x)
 
 
 def test_unit_sphere_rejection_without_sqrt():
