@@ -123,6 +123,10 @@ typedef struct lrt_render_desc {
                                 whose path ends takes the wave's next pixel-sample at once;
                                 colours are lerped in frame order per pixel when the pool
                                 is done. No lrt_features.                             */
+#define LRT_F_BVH 1024       /* closest hits through the 4-wide BVH even where the library
+                                would pick the uniform grid (scenes above 16 spheres) */
+#define LRT_F_GRID 2048      /* closest hits through the uniform grid (lrt_grid.h) even where
+                                the library would pick the BVH; same bits either way */
 
 /* ---- the reference API (parallel.h:6-8) ---------------------------------- */
 
@@ -300,6 +304,14 @@ int lrt_libm_eval_device(int kind, const float* d_in, float* d_out, long long n)
  * traversal-stack entry any of those traversals wrote, and the entries the device's LDS
  * stack holds for this scene (the first must not exceed the second). */
 int lrt_bvh_stats(const lrt_sphere* spheres, int count, const float* rays, int n, double* out);
+/* Diagnostic (host only, no GPU): the uniform grid (lrt_grid.h) of the given scene, built as
+ * lrt_set_scene would, traced for n rays (o.xyz, d.xyz; d normalised as the Ray ctor does) by
+ * the device's walk compiled for the host. out[0..9]: mean cells visited, mean spheres tested,
+ * max (cells + spheres) of one ray, fraction of rays whose closest (id, t), bounded shadow answer
+ * or two-query result differs from the linear scan (must be 0), fraction of rays that took the
+ * fallback scan, cells per axis (3), spheres tested first by every ray, and 1 when the library
+ * would pick the grid for this scene (LRT_ACCEL=auto). */
+int lrt_grid_stats(const lrt_sphere* spheres, int count, const float* rays, int n, double* out);
 /* Closest hit of n rays (6 floats each; d normalised as the Ray ctor does) through the BVH
  * of the given scene: ids[i] (-1: miss) and ts[i]. mode 0: host build of the per-lane
  * traversal; 1: the same on the device (one thread per ray); 2: the device's packet

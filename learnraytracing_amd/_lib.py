@@ -131,6 +131,7 @@ SIGNATURES = {
     "lrt_libm_eval_host": (_i, [_i, _vp, _vp, _c.c_longlong]),
     "lrt_libm_eval_device": (_i, [_i, _vp, _vp, _c.c_longlong]),
     "lrt_bvh_stats": (_i, [_c.POINTER(Sphere), _i, _vp, _i, _vp]),
+    "lrt_grid_stats": (_i, [_c.POINTER(Sphere), _i, _vp, _i, _vp]),
     "lrt_bvh_eval": (_i, [_c.POINTER(Sphere), _i, _vp, _i, _vp, _vp, _i]),
     "lrt_scatter_eval": (_i, [_c.POINTER(Sphere), _c.POINTER(Material), _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp,
                               _vp, _i]),

@@ -1,0 +1,270 @@
+// Bit-exact uniform-grid closest hit (BASELINE configs 4-5).
+//
+// The same exactness argument as the BVH (lrt_bvh.h): for sphere i the reference's HitSphere
+// arithmetic gives a candidate cand_i (first root if > tMin, else the second, else +inf)
+// independent of closestT, and HitWorld's scan (parallel.cpp:54-73, maths.cpp:51-94) returns
+// the lexicographic minimum of (cand_i, i). Any traversal that evaluates the same per-sphere
+// arithmetic for every sphere that could win and keeps that minimum returns the same bits.
+//
+// The grid: a box over the scene's spheres split into n.x * n.y * n.z cells; each sphere is
+// listed in every cell its bounding box, padded by `pad`, overlaps (CSR: cells[c] ..
+// cells[c + 1] index cell-ordered copies of the spheres and their original indices). Spheres
+// that would make the box or the cells large (the r = 100 ground, the light above the
+// others) are tested first by every ray instead, as the BVH does with its `big` spheres.
+// A ray walks the cells it crosses in order (3D DDA, Amanatides & Woo) from where it enters
+// the box. The walk stops once the best candidate lies before the exit of the current cell:
+// every ray point up to that exit lies within the DDA's rounding error of a visited cell, a
+// sphere's hit point lies in its box, and the box was padded by more than that error -- so a
+// sphere not yet tested has cand > the exit >= best and can neither win nor tie. Rays whose
+// rounding bound (from |origin| and the entry distance) exceeds the padding's share scan every
+// sphere instead (never in practice). No stack: the walk's state is a cell and three plane
+// times, so the traversal holds fewer registers than the BVH's and no LDS.
+//
+// Walk and sphere tests share ONE loop (GridStep): an iteration advances to the next cell
+// when the current cell's list is used up, then tests one sphere. A wave therefore runs max
+// over lanes of (cells + spheres) iterations, not the sum of per-cell maxima.
+#pragma once
+
+namespace lrt {
+
+struct GridView {
+    const unsigned* cells;   // ncells + 1 offsets into rsph / rid
+    const float4* rsph;      // cell-ordered sphere copies: float4(center, r^2)
+    const int* rid;          // their original indices
+    const float4* bsph;      // spheres every ray tests first
+    const int* bid;
+    const float4* all;       // the scene in index order (the fallback scan)
+    int nbig, count;
+    int nx, ny, nz;
+    float lox, loy, loz;     // the box's low corner
+    float hx, hy, hz;        // cell size per axis
+    float ihx, ihy, ihz;     // 1 / cell size
+    float pad;               // insertion padding (absolute)
+    float errk;              // a ray may walk if 2^-18 (max|o| + tEnter + ext) < errk (= pad / 2)
+    float ext;               // max |coordinate| of the box
+    int on;
+};
+
+// Host diagnostics (lrt_grid_stats): cell steps, sphere tests and fallback scans.
+struct GridStats { int cells = 0, spheres = 0, fallback = 0; };
+
+// One query's walk. best: the winner's original index; -1 none; -2 the light (shadow query).
+struct GridQuery {
+    F3 o, d, db;      // origin, this query's direction, the bounce query's direction (dual)
+    F3 inv;           // 1 / d
+    float tnx, tny, tnz;   // each axis' next plane crossing
+    float bestT;
+    int best, li;
+    int cx, cy, cz;   // current cell
+    unsigned j, jend; // the current cell's sphere range still to test
+    int mode;         // 0 walking, 1 scanning every sphere (fallback), 2 this query is over
+    bool sh, lit, busy;
+};
+
+LRT_DEV float GridPlane(float lo, int c, float h) { return lo + (float)c * h; }
+
+// (cand, index) order: does sphere `id` with candidate cand beat the query's best?
+LRT_DEV bool GridBeats(const GridQuery& q, float cand, int id) {
+    return cand < q.bestT || (cand == q.bestT && q.best != -1 && id < (q.best >= 0 ? q.best : q.li));
+}
+LRT_DEV float GridCand(const F3& o, const F3& d, const float4& s) {   // maths.cpp:54-90
+    const F3 rs = f3(s.x, s.y, s.z) - o;
+    const float rsProj = dot(rs, d);
+    const float ifHit = dot(rs, rs) - rsProj * rsProj - s.w;
+    if (!(ifHit < 0.0f)) return __builtin_inff();
+    const float halfCut = sqrt_rn(-ifHit);
+    const float t1 = rsProj - halfCut;
+    const float t2 = rsProj + halfCut;
+    return t1 > kMinT ? t1 : (t2 > kMinT ? t2 : __builtin_inff());
+}
+LRT_DEV void GridTest(GridQuery& q, const float4& s, int id) {
+    const float cand = GridCand(q.o, q.d, s);
+    if (GridBeats(q, cand, id)) {
+        q.bestT = cand;
+        q.best = id;
+    }
+}
+
+// Starts q's walk along q.d (q.bestT / q.best / q.li set by the caller): the big spheres,
+// then the cell where the ray enters the box.
+LRT_DEV void GridStart(GridQuery& q, const GridView& g, GridStats* st = nullptr) {
+    for (int k = 0; k < g.nbig; ++k) GridTest(q, g.bsph[k], g.bid[k]);
+    q.inv = f3(rcp_rn(q.d.x), rcp_rn(q.d.y), rcp_rn(q.d.z));
+    q.mode = 2;
+    if (g.count == 0 || g.nx == 0) return;
+    const float hix = GridPlane(g.lox, g.nx, g.hx), hiy = GridPlane(g.loy, g.ny, g.hy),
+                hiz = GridPlane(g.loz, g.nz, g.hz);
+    // the box's slab interval; an axis the ray does not move along constrains through o
+    float t0 = 0.0f, t1 = __builtin_inff();
+    auto slab = [&](float o, float d, float inv, float lo, float hi) {
+        if (d == 0.0f) {
+            if (o < lo || o > hi) t1 = -1.0f;
+            return;
+        }
+        const float a = (lo - o) * inv, b = (hi - o) * inv;
+        t0 = __builtin_fmaxf(t0, __builtin_fminf(a, b));
+        t1 = __builtin_fminf(t1, __builtin_fmaxf(a, b));
+    };
+    slab(q.o.x, q.d.x, q.inv.x, g.lox, hix);
+    slab(q.o.y, q.d.y, q.inv.y, g.loy, hiy);
+    slab(q.o.z, q.d.z, q.inv.z, g.loz, hiz);
+    // (a NaN from a huge origin fails every compare below: the fallback scan takes it)
+    const float slack = g.pad + 1e-5f * t1;
+    if (t0 > t1 + slack || q.bestT < t0 - g.pad - 1e-5f * t0) return;   // misses the box, or beaten before it
+    const float mo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(q.o.x), __builtin_fabsf(q.o.y)),
+                                     __builtin_fabsf(q.o.z));
+    if (!((mo + t0 + g.ext) * 3.814697265625e-06f < g.errk)) {   // 2^-18: the walk's rounding bound
+        if (st) st->fallback += 1;
+        q.mode = 1;
+        q.j = 0;
+        q.jend = (unsigned)g.count;
+        return;
+    }
+    const F3 p = q.o + q.d * t0;
+    auto cell = [](float p, float lo, float ih, int n) {
+        const float f = (p - lo) * ih;
+        int c = f >= 0.0f ? (int)f : 0;
+        return c < n ? c : n - 1;
+    };
+    q.cx = cell(p.x, g.lox, g.ihx, g.nx);
+    q.cy = cell(p.y, g.loy, g.ihy, g.ny);
+    q.cz = cell(p.z, g.loz, g.ihz, g.nz);
+    q.tnx = q.d.x > 0.0f ? (GridPlane(g.lox, q.cx + 1, g.hx) - q.o.x) * q.inv.x
+            : q.d.x < 0.0f ? (GridPlane(g.lox, q.cx, g.hx) - q.o.x) * q.inv.x : __builtin_inff();
+    q.tny = q.d.y > 0.0f ? (GridPlane(g.loy, q.cy + 1, g.hy) - q.o.y) * q.inv.y
+            : q.d.y < 0.0f ? (GridPlane(g.loy, q.cy, g.hy) - q.o.y) * q.inv.y : __builtin_inff();
+    q.tnz = q.d.z > 0.0f ? (GridPlane(g.loz, q.cz + 1, g.hz) - q.o.z) * q.inv.z
+            : q.d.z < 0.0f ? (GridPlane(g.loz, q.cz, g.hz) - q.o.z) * q.inv.z : __builtin_inff();
+    const int c = (q.cz * g.ny + q.cy) * g.nx + q.cx;
+    q.j = g.cells[c];
+    q.jend = g.cells[c + 1];
+    q.mode = 0;
+    if (st) st->cells += 1;
+}
+
+// One iteration of q's query: the next cell if the current one is used up (or the end of the
+// walk), then one sphere test.
+LRT_DEV void GridAdvance(GridQuery& q, const GridView& g, GridStats* st) {
+    if (q.mode != 0 || q.j < q.jend) return;
+    const float T = __builtin_fminf(__builtin_fminf(q.tnx, q.tny), q.tnz);
+    if (q.bestT < T - (g.pad + 1e-5f * T)) {   // nothing beyond this cell can win or tie
+        q.mode = 2;
+        return;
+    }
+    if (q.tnx == T) {
+        q.cx += q.d.x > 0.0f ? 1 : -1;
+        if ((unsigned)q.cx >= (unsigned)g.nx) { q.mode = 2; return; }
+        q.tnx = (GridPlane(g.lox, q.cx + (q.d.x > 0.0f ? 1 : 0), g.hx) - q.o.x) * q.inv.x;
+    } else if (q.tny == T) {
+        q.cy += q.d.y > 0.0f ? 1 : -1;
+        if ((unsigned)q.cy >= (unsigned)g.ny) { q.mode = 2; return; }
+        q.tny = (GridPlane(g.loy, q.cy + (q.d.y > 0.0f ? 1 : 0), g.hy) - q.o.y) * q.inv.y;
+    } else {
+        if (!(q.tnz == T)) { q.mode = 2; return; }   // all three infinite / NaN: nowhere to go
+        q.cz += q.d.z > 0.0f ? 1 : -1;
+        if ((unsigned)q.cz >= (unsigned)g.nz) { q.mode = 2; return; }
+        q.tnz = (GridPlane(g.loz, q.cz + (q.d.z > 0.0f ? 1 : 0), g.hz) - q.o.z) * q.inv.z;
+    }
+    const int c = (q.cz * g.ny + q.cy) * g.nx + q.cx;
+    q.j = g.cells[c];
+    q.jend = g.cells[c + 1];
+    if (st) st->cells += 1;
+}
+LRT_DEV void GridIter(GridQuery& q, const GridView& g, GridStats* st) {
+    GridAdvance(q, g, st);
+    if (q.mode != 2 && q.j < q.jend) {
+        if (st) st->spheres += 1;
+        const unsigned j = q.j++;
+        if (q.mode == 0) {
+            const float4 s = g.rsph[j];
+            const float cand = GridCand(q.o, q.d, s);
+            // the original index is read only when it can matter (a win or an exact tie)
+            if (cand < q.bestT || (cand == q.bestT && q.best != -1)) {
+                const int id = g.rid[j];
+                if (GridBeats(q, cand, id)) {
+                    q.bestT = cand;
+                    q.best = id;
+                }
+            }
+        } else {
+            GridTest(q, g.all[j], (int)j);
+            if (q.j >= q.jend) q.mode = 2;
+        }
+    } else if (q.mode == 1) {
+        q.mode = 2;
+    }
+}
+
+LRT_DEV int ClosestHitGrid(const F3& o, const F3& d, const GridView& g, float& tOut, GridStats* st = nullptr) {
+    GridQuery q;
+    q.o = o;
+    q.d = d;
+    q.bestT = kMaxT;
+    q.best = -1;
+    q.li = -1;
+    GridStart(q, g, st);
+    while (q.mode != 2) GridIter(q, g, st);
+    tOut = q.bestT;
+    return q.best;
+}
+
+// `HitWorld(shadow ray) && hitID == li` (parallel.cpp:122-123): the closest-hit query with the
+// light's own (cand, li) as the bar from the start; the first sphere that beats it ends it.
+LRT_DEV bool ShadowReachesLightGrid(const F3& o, const F3& d, int li, const float4& lightSph, const GridView& g,
+                                    GridStats* st = nullptr) {
+    const float candL = GridCand(o, d, lightSph);
+    if (!(candL < kMaxT)) return false;
+    GridQuery q;
+    q.o = o;
+    q.d = d;
+    q.bestT = candL;
+    q.best = -2;
+    q.li = li;
+    GridStart(q, g, st);
+    while (q.mode != 2 && q.best == -2) GridIter(q, g, st);
+    return q.best == -2;
+}
+
+// The pool kernel's two queries from one origin in one loop (as ClosestHitDualBVH4): the
+// deferred shadow ray of the last light (when hasS), then the bounce ray's closest hit.
+LRT_DEV void GridDualInit(GridQuery& q, const F3& o, const F3& db, bool hasS, const F3& ds, int li,
+                          const float4& lightSph, const GridView& g, GridStats* st) {
+    q.o = o;
+    q.db = db;
+    q.li = li;
+    q.lit = false;
+    q.busy = true;
+    const float candL = hasS ? GridCand(o, ds, lightSph) : kMaxT;
+    q.sh = candL < kMaxT;   // no shadow ray, or the light is not hit at all: not lit
+    q.d = q.sh ? ds : db;
+    q.bestT = q.sh ? candL : kMaxT;
+    q.best = q.sh ? -2 : -1;
+    GridStart(q, g, st);
+}
+LRT_DEV void GridDualStep(GridQuery& q, const GridView& g, GridStats* st) {
+    GridIter(q, g, st);
+    const bool qdone = q.mode == 2 || (q.sh && q.best != -2);
+    if (qdone) {
+        if (q.sh) {
+            q.lit = q.best == -2;   // nothing beat the light
+            q.sh = false;
+            q.d = q.db;
+            q.bestT = kMaxT;
+            q.best = -1;
+            GridStart(q, g, st);
+        } else {
+            q.busy = false;
+        }
+    }
+}
+LRT_DEV int ClosestHitDualGrid(const F3& o, const F3& db, bool hasS, const F3& ds, int li, const float4& lightSph,
+                               const GridView& g, float& tOut, bool& lit, GridStats* st = nullptr) {
+    GridQuery q;
+    GridDualInit(q, o, db, hasS, ds, li, lightSph, g, st);
+    while (q.busy) GridDualStep(q, g, st);
+    lit = q.lit;
+    tOut = q.bestT;
+    return q.best;
+}
+
+}  // namespace lrt

@@ -24,13 +24,6 @@
 
 namespace lrt {
 
-// Samples per round of a tile, at most: with pixels x frames <= kPoolSamples a tile has one
-// round. Config 4 (64 spp): 1024 (16 px) 229 ms, 2048 (32 px) 222, 4096 (64 px) 221;
-// config 5 (256 spp, one GPU): 1024 (4 px) 3876 ms, 4096 (16 px) 3602 (profiles/r2_p2).
-#ifndef LRT_POOL_SAMPLES
-#define LRT_POOL_SAMPLES 4096
-#endif
-constexpr int kPoolSamples = LRT_POOL_SAMPLES;
 #ifndef LRT_POOL_PACKET
 #define LRT_POOL_PACKET 0
 #endif
@@ -60,11 +53,11 @@ typedef const KernelArgs* KArgPtr;
 __device__ __forceinline__ KArgPtr opaque_args() { return nullptr; }
 #endif
 
-template <int MAXD, bool kLds, bool kBvh, int kPix, int kNS = 0>
+template <int MAXD, bool kLds, int kAcc, int kPix, int kNS = 0>
 __global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const KernelArgs a) {
-    static_assert(kNS == 0 || (kLds && !kBvh), "a fixed sphere count is for the LDS linear scan");
+    static_assert(kNS == 0 || (kLds && !kAcc), "a fixed sphere count is for the LDS linear scan");
     // LDS as trace_kernel: [recursion stack kTraceLdsLevels x 64][powf tables][renormalize
-    // table unless kBvh][spheres][materials][lights][bvh stack at a.bvh_stack_offset]
+    // table unless kAcc][spheres][materials][lights][bvh stack at a.bvh_stack_offset]
     extern __shared__ float4 smem[];
     const int lane = threadIdx.x;
     double* s_pow = reinterpret_cast<double*>(smem + kTraceLdsLevels * 64);
@@ -76,9 +69,9 @@ __global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const Ker
         }
         for (int i = lane; i < 32; i += 64) reinterpret_cast<uint64_t*>(s_pow + 32)[i] = g.exp2[i];
     }
-    constexpr int kLutBytes = kBvh ? 0 : kRenormBytes;
-    float* s_lut = kBvh ? nullptr : reinterpret_cast<float*>(s_pow + 64);
-    if (!kBvh) renorm_lut_fill(s_lut, lane, 64);
+    constexpr int kLutBytes = kAcc ? 0 : kRenormBytes;
+    float* s_lut = kAcc ? nullptr : reinterpret_cast<float*>(s_pow + 64);
+    if (!kAcc) renorm_lut_fill(s_lut, lane, 64);
     float4* s_sph = smem + kTraceLdsLevels * 64 + (kPowTableBytes + kLutBytes) / 16;
     float4* s_mat = s_sph + a.count;
     int* s_lights = reinterpret_cast<int*>(s_mat + 3 * a.count);
@@ -99,6 +92,7 @@ __global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const Ker
     sc.count = a.count;
     sc.nlights = a.nlights;
     sc.bv = a.bv;
+    sc.gv = a.gv;
     sc.bstk = reinterpret_cast<unsigned short*>(reinterpret_cast<char*>(smem) + a.bvh_stack_offset) + lane;
     sc.bstride = 64;
 #ifdef LRT_EXP_SECSTATS
@@ -223,7 +217,7 @@ __global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const Ker
                 // iteration) take the packet traversal (lrt_bvh.h). Off: without the packet
                 // code the instance keeps its traversal state in fewer registers (config 4:
                 // 222.4 -> 209.8 ms/step, profiles/r2_q2)
-                const bool coherent = kBvh && LRT_POOL_PACKET && LRT_PACKET_DEPTH > 0 &&
+                const bool coherent = kAcc == kAccBvh && LRT_POOL_PACKET && LRT_PACKET_DEPTH > 0 &&
                                       __ballot(state == kPoolTrace && depth != 0) == 0 &&
                                       __ballot(state == kPoolTrace && pend) == 0;
                 sec_enter(sc, kSecOther, false);
@@ -236,7 +230,10 @@ __global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const Ker
                     float nt;
                     bool lit = false;
                     const bool hasS = pend && dl.on;
-                    if constexpr (kBvh) {
+                    if constexpr (kAcc == kAccGrid) {
+                        const float4 ls = hasS ? sc.sph[dl.li] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                        nid = ClosestHitDualGrid(r.orig, r.dir, hasS, dl.l, dl.li, ls, sc.gv, nt, lit);
+                    } else if constexpr (kAcc == kAccBvh) {
                         if (coherent) {
                             nid = ClosestHitBVH(r.orig, r.dir, sc.bv, nt, sc.bstk, sc.bstride, nullptr, true);
                         } else {
@@ -273,7 +270,7 @@ __global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const Ker
                         if (depth < a.maxDepth) {
                             F3 lightE;
                             dl.on = false;
-                            const F3 X = ScatterDir<kBvh, kNS>(mat, nid, r, rec, lightE, rays, rng, sc, &dl, coherent);
+                            const F3 X = ScatterDir<kAcc, kNS>(mat, nid, r, rec, lightE, rays, rng, sc, &dl, coherent);
                             sec_count(sc, kSecPost);
                             const F3 dir = renormalize(normalize(X), sc.rnlut);   // Ray(rec.pos, normalize(X))
                             if (mat.type != 1 || dot(dir, rec.normal) > 0.0f) {    // Metal absorbs (:147)
@@ -361,112 +358,6 @@ __global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const Ker
 #endif
     const unsigned long long total = wave_sum((unsigned long long)rays);
     if (lane == 0) block_epilogue(a.tiles, a.rays, q, bq, total);
-}
-
-// ---- first launch of a view: a cost probe instead of queue order ------------------------
-// The heaviest-first order (tile_order) needs each tile's cost. Until a launch of the render
-// signature has measured them, a probe estimates them: kProbe camera rays per tile (a 4x4
-// grid over the tile, the launch's first frame, the real camera and seeds), each weighted by
-// what its first hit costs a path on average -- the sky ends the path at once, a Lambert
-// surface scatters and samples its lights, metal reflects, glass refracts into long chains.
-// One closest hit per probe ray, 4 tiles per wave: ~1/16 of a 64-px, 4-spp tile's camera
-// rays and none of its bounces. probe_order_kernel then counting-sorts the tiles by
-// descending key in one workgroup. Only the order in which the render takes its tiles
-// changes, never a pixel; the render still records its measured costs for later launches.
-constexpr int kProbe = 16;
-constexpr unsigned kProbeW[4] = {1u, 3u, 4u, 8u};   // sky, Lambert, Metal, Dielectric
-constexpr unsigned kProbeKeyMax = kProbe * 8u;
-template <bool kBvh>
-__global__ __launch_bounds__(64) void probe_kernel(const KernelArgs a, unsigned* key, int ntiles, int TX, int TY) {
-    extern __shared__ float4 smem[];
-    const int lane = threadIdx.x;
-    SceneView sc;
-    sc.rnlut = nullptr;
-    sc.sph = a.sph;
-    sc.mats = a.mats;
-    sc.lights = a.lights;
-    sc.count = a.count;
-    sc.nlights = a.nlights;
-    sc.bv = a.bv;
-    sc.bstk = reinterpret_cast<unsigned short*>(smem) + lane;
-    sc.bstride = 64;
-    const int tile = blockIdx.x * (64 / kProbe) + lane / kProbe, k = lane % kProbe;
-    const int tilesX = (a.xc + TX - 1) / TX;
-    const int lx = (tile % tilesX) * TX + (k % 4) * TX / 4 + TX / 8;
-    const int ly = (tile / tilesX) * TY + (k / 4) * TY / 4 + TY / 8;
-    unsigned w = 0;
-    if (tile < ntiles && lx < a.xc && ly < a.rows) {
-        const int x = a.x0 + lx, y = GlobalRow(a, ly);
-        uint32_t rng = PixelSeed((uint32_t)x, (uint32_t)y, (uint32_t)a.frame0);
-        const float u = ((float)x + RandomFloat01(rng)) * (1.0f / (float)a.width);
-        const float v = ((float)y + RandomFloat01(rng)) * (1.0f / (float)a.height);
-        const Ray r = GetRay(a.cam, u, v, rng, nullptr);
-        float t;
-        const int id = ClosestHitSV<kBvh, 0>(r, kMinT, kMaxT, sc, t);
-        const int type = id < 0 ? -1 : libm::f2u_i(a.mats[3 * id].w);
-        w = kProbeW[type < 0 ? 0 : type > 2 ? 3 : type + 1];
-    }
-    for (int off = 1; off < kProbe; off <<= 1) w += __shfl_xor(w, off, 64);
-    if (tile < ntiles && k == 0) key[tile] = w;
-}
-// One workgroup: per-wave histograms of the keys in LDS (16 copies, so the few distinct keys
-// do not serialise every atomic on one address), bucket starts in descending key order
-// across the copies, then every tile to its wave's share of its bucket (order within a
-// bucket is whatever the LDS atomics give).
-__global__ __launch_bounds__(1024) void probe_order_kernel(const unsigned* key, int* perm, int n) {
-    constexpr int kB = kProbeKeyMax + 1, kW = 16;
-    __shared__ unsigned hist[kW][kB];
-    const int w = threadIdx.x >> 6;
-    for (int i = threadIdx.x; i < kW * kB; i += 1024) (&hist[0][0])[i] = 0;
-    __syncthreads();
-    // 16 independent loads in flight per thread and pass (one at a time, the passes were
-    // load-latency bound: 22 us for 14,400 tiles)
-    for (int base = 0; base < n; base += 16 * 1024) {
-        unsigned k[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int i = base + j * 1024 + (int)threadIdx.x;
-            k[j] = i < n ? min(key[i], kProbeKeyMax) : kB;
-        }
-#pragma unroll
-        for (int j = 0; j < 16; ++j)
-            if (k[j] < (unsigned)kB) atomicAdd(&hist[w][k[j]], 1u);
-    }
-    __syncthreads();
-    if (threadIdx.x < 64) {   // one wave: bucket b's totals, descending exclusive scan
-        unsigned run = 0;
-        for (int b0 = kB - 1; b0 >= 0; b0 -= 64) {
-            const int b = b0 - (int)threadIdx.x;
-            unsigned tot = 0;
-            if (b >= 0)
-                for (int c = 0; c < kW; ++c) tot += hist[c][b];
-            unsigned inc = tot;   // inclusive scan over the lanes (descending b)
-            for (int off = 1; off < 64; off <<= 1) {
-                const unsigned o = __shfl_up(inc, off, 64);
-                if ((int)threadIdx.x >= off) inc += o;
-            }
-            unsigned base = run + inc - tot;
-            if (b >= 0)
-                for (int c = 0; c < kW; ++c) {
-                    const unsigned v = hist[c][b];
-                    hist[c][b] = base;
-                    base += v;
-                }
-            run += __shfl(inc, 63, 64);
-        }
-    }
-    __syncthreads();
-    for (int base = 0; base < n; base += 16 * 1024) {
-        unsigned k[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int i = base + j * 1024 + (int)threadIdx.x;
-            k[j] = i < n ? min(key[i], kProbeKeyMax) : kB;
-        }
-#pragma unroll
-        for (int j = 0; j < 16; ++j)
-            if (k[j] < (unsigned)kB) perm[atomicAdd(&hist[w][k[j]], 1u)] = base + j * 1024 + (int)threadIdx.x;
-    }
 }
 
 }  // namespace lrt

@@ -1,0 +1,149 @@
+// The pool kernel's launch (lrt_pool.h): grid, colour slots, overflow stack, tile order.
+// Instantiated per depth class by lrt_pool_d8.hip and lrt_pool_d64.hip.
+#pragma once
+#include "lrt_internal.h"
+#include "lrt_pool.h"
+
+namespace lrt {
+
+template <int MAXD, int kPix>
+int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
+    constexpr int TX = PoolTile<kPix>::X, TY = PoolTile<kPix>::Y;
+    const long long ntiles = (long long)((xc + TX - 1) / TX) * ((rows + TY - 1) / TY);
+    const size_t stack = sizeof(float4) * kTraceLdsLevels * 64 + kPowTableBytes + (a.bv.on ? 0 : kRenormBytes);
+    const size_t scene = lds ? sizeof(float4) * (4 * (size_t)a.count + (size_t)(a.nlights + 3) / 4 + 1) : 0;
+    a.bvh_stack_offset = (int)(stack + scene);
+    const int acc = a.gv.on ? kAccGrid : a.bv.on ? kAccBvh : kAccScan;
+    const size_t bstk = acc == kAccBvh ? sizeof(unsigned short) * ctx().bvh_stack_levels * 64 : 0;
+    const size_t ldsb = stack + scene + bstk;
+    const bool fixed = lds && !a.bv.on && a.count == kFixedSpheres;
+    const void* kern = acc == kAccGrid ? (lds ? (const void*)pool_kernel<MAXD, true, kAccGrid, kPix>
+                                              : (const void*)pool_kernel<MAXD, false, kAccGrid, kPix>)
+                       : acc == kAccBvh ? (lds ? (const void*)pool_kernel<MAXD, true, kAccBvh, kPix>
+                                               : (const void*)pool_kernel<MAXD, false, kAccBvh, kPix>)
+                       : (fixed ? (const void*)pool_kernel<MAXD, true, kAccScan, kPix, kFixedSpheres>
+                          : lds ? (const void*)pool_kernel<MAXD, true, kAccScan, kPix>
+                                : (const void*)pool_kernel<MAXD, false, kAccScan, kPix>);
+    int per_cu = 0;
+    hipError_t e = occupancy(&per_cu, kern, 64, ldsb);
+    if (e != hipSuccess) return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
+    if (per_cu < 1) return fail(LRT_E_INVALID, "pool_kernel does not fit on a CU");
+    int cus = ctx().num_cus;
+    for (const auto& m : ctx().masked_streams)
+        if (m.first == s) cus = m.second;
+    long long blocks = std::max((long long)per_cu * cus, (long long)kV0Queues);   // a block per queue (as v0)
+    if (blocks > ntiles) blocks = ntiles;
+    const dim3 grid((unsigned)blocks);
+    a.ovf = nullptr;
+    a.colbuf = nullptr;
+    a.tiles = ctx().d_tiles + (size_t)(ctx().tiles_next++ % kQueueSlots) * kTileSetU64;
+    {   // waiting lanes that trigger a refill (fold + next samples); LRT_POOL_REFILL_MIN.
+        // Measured (profiles/r2_p2): config 3 2.31 -> 2.05 ms/step at 16 (vs 1), config 4 and
+        // config 2 neutral
+        static int env = -1;
+        if (env < 0) {
+            const char* v = getenv("LRT_POOL_REFILL_MIN");
+            env = v ? atoi(v) : 0;
+            if (env <= 0 || env > 64) env = 16;
+        }
+        a.regenMin = env;
+    }
+    a.poolSlots = kPix * std::min(a.frames, kPoolSamples / kPix);   // one round's samples
+    e = hipMallocAsync((void**)&a.colbuf, sizeof(float4) * (size_t)a.poolSlots * grid.x, s);
+    if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(pool colour slots)");
+    if (a.maxDepth > kTraceLdsLevels) {
+        const size_t gthreads = (size_t)grid.x * 64;
+        e = hipMallocAsync((void**)&a.ovf, sizeof(float4) * gthreads * (size_t)(a.maxDepth - kTraceLdsLevels), s);
+        if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(trace stack overflow)");
+    }
+#ifdef LRT_EXP_SECSTATS
+    unsigned long long* d_sec = secstats_buffer(s);
+    a.wtrace = d_sec;
+#endif
+#ifdef LRT_EXP_WAVETRACE
+    a.wtrace = wavetrace_buffer(grid.x);
+#endif
+    bool record = false;
+    Context::TileOrder* users[2];
+    if (int rc = tile_order(a, kPix, ntiles, record, users, s)) return rc;
+    bool probed = false;
+    if (record && pool_probe_mode() > 0 && (pool_probe_mode() == 2 || !users[1])) {
+        // no measured order to go by: probe the tiles' costs, sort them, and let this
+        // (recording) launch take its tiles in that order (probe_kernel, lrt_pool.h)
+        Context::TileOrder& o = *users[0];
+        KernelArgs pa = a;
+        pa.bvh_stack_offset = 0;
+        e = launch_tile_probe(pa, acc, o, (int)ntiles, TX, TY, bstk, s);
+        if (e != hipSuccess) {
+            o.state = 0;
+            return hip_fail(e, "tile cost probe");
+        }
+        a.perm = o.d_perm;
+        users[1] = nullptr;   // (a borrowed order, if any, is not used)
+        probed = true;
+    }
+    if (acc == kAccGrid) {
+        if (lds) pool_kernel<MAXD, true, kAccGrid, kPix><<<grid, 64, ldsb, s>>>(a);
+        else pool_kernel<MAXD, false, kAccGrid, kPix><<<grid, 64, ldsb, s>>>(a);
+    } else if (acc == kAccBvh) {
+        if (lds) pool_kernel<MAXD, true, kAccBvh, kPix><<<grid, 64, ldsb, s>>>(a);
+        else pool_kernel<MAXD, false, kAccBvh, kPix><<<grid, 64, ldsb, s>>>(a);
+    } else if (fixed) {
+        pool_kernel<MAXD, true, kAccScan, kPix, kFixedSpheres><<<grid, 64, ldsb, s>>>(a);
+    } else {
+        if (lds) pool_kernel<MAXD, true, kAccScan, kPix><<<grid, 64, ldsb, s>>>(a);
+        else pool_kernel<MAXD, false, kAccScan, kPix><<<grid, 64, ldsb, s>>>(a);
+    }
+    e = hipGetLastError();
+    if (e != hipSuccess) {
+        if (record) users[0]->state = 0;   // nothing recorded: the entry is free again
+        return hip_fail(e, "pool_kernel launch");
+    }
+    if (record) {   // the costs just recorded, sorted on the device behind the launch
+        Context::TileOrder& o = *users[0];
+        e = sort_tiles_desc(o.d_cost, o.d_keys, o.d_ids, o.d_perm, (int)ntiles, o.d_tmp, &o.tmp_bytes, s);
+        if (e == hipSuccess) e = hipEventRecord(o.ev_rec, s);
+        if (e != hipSuccess) {
+            o.state = 0;   // no order for this signature: the next launch records again
+            return hip_fail(e, "tile order sort");
+        }
+    }
+    for (auto* u : users)
+        if (u)
+            if (int rc = order_used(*u, s)) return rc;
+    // order: 0 queue order (tile order off), 1 recording in queue order, 2 the signature's own
+    // sorted order, 3 recording with the order borrowed from the same geometry, 4 recording in
+    // the probe's order
+    snprintf(g_last_launch, sizeof(g_last_launch),
+             "kernel=pool_kernel maxd=%d lds=%d bvh=%d acc=%s pix=%d ns=%d grid=%u tasks=%lld order=%d per_cu=%d", MAXD,
+             lds ? 1 : 0, acc == kAccBvh ? 1 : 0, acc_name(acc), kPix, fixed ? kFixedSpheres : 0, grid.x, ntiles,
+             !users[0] ? 0 : !record ? 2 : probed ? 4 : users[1] ? 3 : 1, per_cu);
+#ifdef LRT_EXP_SECSTATS
+    secstats_dump(d_sec, s);
+#endif
+#ifdef LRT_EXP_WAVETRACE
+    wavetrace_dump(a.wtrace, grid.x, s);
+#endif
+    e = hipFreeAsync(a.colbuf, s);
+    if (e != hipSuccess) return hip_fail(e, "hipFreeAsync(pool colour slots)");
+    if (a.ovf) {
+        e = hipFreeAsync(a.ovf, s);
+        if (e != hipSuccess) return hip_fail(e, "hipFreeAsync(trace stack overflow)");
+    }
+    return LRT_OK;
+}
+
+template <int MAXD>
+int launch_pool_split(const KernelArgs& a, bool lds, int xc, int rows, int frames, hipStream_t s) {
+    switch (pool_pixels(frames, xc, rows)) {
+        case 256: return launch_pool<MAXD, 256>(a, lds, xc, rows, s);
+        case 128: return launch_pool<MAXD, 128>(a, lds, xc, rows, s);
+        case 64: return launch_pool<MAXD, 64>(a, lds, xc, rows, s);
+        case 32: return launch_pool<MAXD, 32>(a, lds, xc, rows, s);
+        case 16: return launch_pool<MAXD, 16>(a, lds, xc, rows, s);
+        case 4: return launch_pool<MAXD, 4>(a, lds, xc, rows, s);
+        default: return launch_pool<MAXD, 1>(a, lds, xc, rows, s);
+    }
+}
+
+}  // namespace lrt

@@ -211,7 +211,13 @@ LRT_DEV Material load_material(const float4* __restrict__ mats, int id) {
 
 }  // namespace lrt
 #include "lrt_bvh.h"
+#include "lrt_grid.h"
 namespace lrt {
+
+// The closest-hit structure a kernel instance is compiled for (template parameter kAcc): the
+// reference's linear scan, the 4-wide BVH (lrt_bvh.h) or the uniform grid (lrt_grid.h). All
+// three return the scan's bits.
+enum : int { kAccScan = 0, kAccBvh = 1, kAccGrid = 2 };
 
 struct SceneView {
     const float4* sph;                 // LDS or global
@@ -219,7 +225,8 @@ struct SceneView {
     const int* __restrict__ lights;    // emissive sphere ids in index order
     int count;
     int nlights;
-    BvhView bv;                        // bv.on: closest hit by BVH traversal
+    BvhView bv;                        // the BVH (kAcc == kAccBvh)
+    GridView gv;                       // the uniform grid (kAcc == kAccGrid)
     unsigned short* bstk;              // this lane's BVH traversal stack (LDS)
     int bstride;
     libm::PowTables pow;               // powf tables for Dielectric's schlick (LDS copy)
@@ -289,10 +296,12 @@ LRT_DEV void SphereRoots(float rsProj, float ifHit, float tMin, float& closestT,
 // reference overwriting them on every closer hit).
 // kNS > 0: the scene has exactly kNS spheres (the reference's kSphereCount is a compile-time
 // 9, parallel.cpp:27): the scan is fully unrolled with constant LDS offsets.
-template <bool kBvh = false, int kNS = 0>
+template <int kAcc = 0, int kNS = 0>
 LRT_DEV int ClosestHitSV(const Ray& r, float tMin, float tMax, const SceneView& sc, float& tOut,
                          bool coherent = false) {
-    if (kBvh)   // tMin/tMax = kMinT/kMaxT
+    if constexpr (kAcc == kAccGrid)   // tMin/tMax = kMinT/kMaxT
+        return ClosestHitGrid(r.orig, r.dir, sc.gv, tOut);
+    if constexpr (kAcc == kAccBvh)
         return ClosestHitBVH(r.orig, r.dir, sc.bv, tOut, sc.bstk, sc.bstride, nullptr, coherent);
     float closestT = tMax;
     int id = -1;
@@ -332,12 +341,12 @@ LRT_DEV int ClosestHit(const F3& o, const F3& d, const float4* sph, int count, f
     return id;
 }
 
-template <bool kBvh = false, int kNS = 0>
+template <int kAcc = 0, int kNS = 0>
 LRT_DEV bool HitWorld(const Ray& r, float tMin, float tMax, const SceneView& sc, Hit& outHit, int& outID,
                       bool coherent = false) {
     float closestT;
     sec_count(sc, coherent ? kSecHit0 : kSecHit);
-    const int id = ClosestHitSV<kBvh, kNS>(r, tMin, tMax, sc, closestT, coherent);
+    const int id = ClosestHitSV<kAcc, kNS>(r, tMin, tMax, sc, closestT, coherent);
     if (id < 0) return false;
     float4 s = sc.sph[id];
     outHit.pos = point_at(r, closestT);
@@ -366,7 +375,7 @@ struct DeferredLight {
     int id;          // the scattering sphere (pool kernel: its stack entry's material)
 };
 
-template <bool kBvh = false, int kNS = 0>
+template <int kAcc = 0, int kNS = 0>
 LRT_DEV F3 ScatterDir(const Material& mat, int matId, const Ray& r_in, const Hit& rec, F3& outLightE,
                       int& inoutRayCount, uint32_t& rng, const SceneView& sc, DeferredLight* defer = nullptr,
                       bool coherent = false) {
@@ -415,7 +424,9 @@ LRT_DEV F3 ScatterDir(const Material& mat, int matId, const Ray& r_in, const Hit
             }
             sec_count(sc, coherent ? kSecShadow0 : kSecShadow);
             bool lit;
-            if constexpr (kBvh) {
+            if constexpr (kAcc == kAccGrid) {
+                lit = ShadowReachesLightGrid(rec.pos, renormalize(l, sc.rnlut), i, s, sc.gv);
+            } else if constexpr (kAcc == kAccBvh) {
                 Ray sr;
                 sr.orig = rec.pos;
                 sr.dir = renormalize(l, sc.rnlut);
@@ -424,7 +435,7 @@ LRT_DEV F3 ScatterDir(const Material& mat, int matId, const Ray& r_in, const Hit
                 Ray sr;
                 sr.orig = rec.pos;
                 sr.dir = renormalize(l, sc.rnlut);
-                lit = ClosestHitSV<kBvh, kNS>(sr, kMinT, kMaxT, sc, tLight) == i;
+                lit = ClosestHitSV<kAcc, kNS>(sr, kMinT, kMaxT, sc, tLight) == i;
             }
             sec_enter(sc, kSecLambert, false);
             if (lit) {   // HitWorld && hitID == i
@@ -476,10 +487,10 @@ LRT_DEV F3 ScatterDir(const Material& mat, int matId, const Ray& r_in, const Hit
 // (src/cpu/README.md:42, fragmentShader.fs.glsl:175-218). `mat.id` is the material's table
 // index, the reference's `&mat` identity. coherent: the active lanes' shadow rays start
 // together (packet traversal, lrt_bvh.h).
-template <bool kBvh = false, int kNS = 0>
+template <int kAcc = 0, int kNS = 0>
 LRT_DEV bool Scatter(const Material& mat, const Ray& r_in, const Hit& rec, F3& attenuation, Ray& scattered,
                      F3& outLightE, int& inoutRayCount, uint32_t& rng, const SceneView& sc, bool coherent = false) {
-    const F3 X = ScatterDir<kBvh, kNS>(mat, mat.id, r_in, rec, outLightE, inoutRayCount, rng, sc, nullptr, coherent);
+    const F3 X = ScatterDir<kAcc, kNS>(mat, mat.id, r_in, rec, outLightE, inoutRayCount, rng, sc, nullptr, coherent);
     scattered.orig = rec.pos;
     scattered.dir = renormalize(normalize(X), sc.rnlut);   // Ray(rec.pos, normalize(X))
     attenuation = mat.att;                                  // albedo, or (1, 1, 1) for Dielectric (:192)
@@ -507,10 +518,10 @@ LRT_DEV F3 TraceDual(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, con
 // 456-457) -- a scatter event reached through a Lambert bounce adds no emissive; the
 // terminating hit always does. kFeat: feat[0..2] receive the first hit's normal,
 // position and albedo (fragmentShader.fs.glsl:444-451; left untouched on a miss).
-template <int MAXD, bool kBvh = false, bool kFeat = false, int kLdsLev = kTraceLdsLevels, int kNS = 0>
+template <int MAXD, int kAcc = 0, bool kFeat = false, int kLdsLev = kTraceLdsLevels, int kNS = 0>
 LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const SceneView& sc,
                  float4* lstk, int lstride, float4* gstk, size_t gstride, int ndl = 0, F3* feat = nullptr) {
-    if constexpr (!kBvh && LRT_DUAL_HIT)
+    if constexpr (!kAcc && LRT_DUAL_HIT)
         return TraceDual<MAXD, kFeat, kLdsLev, kNS>(r, maxDepth, inoutRayCount, rng, sc, lstk, lstride, gstk, gstride,
                                                ndl, feat);
     auto put = [&](int lvl, float4 v) {
@@ -530,7 +541,7 @@ LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const S
         ++inoutRayCount;
         // the first rays of a wave's paths start together: packet traversal (lrt_bvh.h)
         const bool coherent = depth < LRT_PACKET_DEPTH;
-        if (!HitWorld<kBvh, kNS>(r, kMinT, kMaxT, sc, rec, id, coherent)) {
+        if (!HitWorld<kAcc, kNS>(r, kMinT, kMaxT, sc, rec, id, coherent)) {
             float t = 0.5f * (r.dir.y + 1.0f);
             leaf = ((1.0f - t) * f3(1.0f, 1.0f, 1.0f) + t * f3(0.5f, 0.7f, 1.0f)) * 0.3f;
             break;
@@ -546,7 +557,7 @@ LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const S
         Ray scattered;
         // :212 -- the attenuation is the material's `att` row, which the fold reads back by id
         if (depth < maxDepth &&
-            Scatter<kBvh, kNS>(mat, r, rec, attenuation, scattered, lightE, inoutRayCount, rng, sc, coherent)) {
+            Scatter<kAcc, kNS>(mat, r, rec, attenuation, scattered, lightE, inoutRayCount, rng, sc, coherent)) {
             sec_count(sc, kSecPost);
             if (ndl && prevLambert) matE = f3(0.0f, 0.0f, 0.0f);
             prevLambert = mat.type == 0;

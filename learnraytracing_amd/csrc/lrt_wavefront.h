@@ -56,7 +56,7 @@ struct WfArgs {
 
 // Scene staging for the wavefront kernels: [powf tables][renormalize table][spheres]
 // [materials][lights][bvh traversal stack]; no recursion stack (it lives in HBM).
-template <bool kBvh>
+template <int kAcc>
 __device__ __forceinline__ SceneView wf_scene(const KernelArgs& a, bool lds, int bstk_off, float4* smem, int tid) {
     double* s_pow = reinterpret_cast<double*>(smem);
     {
@@ -163,10 +163,10 @@ __global__ __launch_bounds__(kWfBlock) void wf_camera(const WfArgs w) {
     if (threadIdx.x == 0) w.cnt[j] = (unsigned int)nj;
 }
 
-template <bool kBvh, int kNS>
+template <int kAcc, int kNS>
 __global__ __launch_bounds__(kWfBlock) void wf_extend(const WfArgs w, int it) {
     extern __shared__ float4 smem[];
-    const SceneView sc = wf_scene<kBvh>(w.a, w.lds != 0, w.bstk_off, smem, threadIdx.x);
+    const SceneView sc = wf_scene<kAcc>(w.a, w.lds != 0, w.bstk_off, smem, threadIdx.x);
     const int B = gridDim.x, j = blockIdx.x;
     const unsigned int n = w.cnt[(size_t)(4 * it) * B + j];
     const uint32_t* q = w.qa[it & 1] + (size_t)j * w.R0;
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_extend(const WfArgs w, int it) {
             ++rays;
             int nid;
             float nt;
-            if constexpr (kBvh) {
+            if constexpr (kAcc) {
                 nid = ClosestHitBVH(org, dir, sc.bv, nt, sc.bstk, sc.bstride);
             } else {
                 const float4 s4 = (flags & 2) ? w.sl[p] : make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
@@ -228,10 +228,10 @@ __global__ __launch_bounds__(kWfBlock) void wf_extend(const WfArgs w, int it) {
     wf_rays(w, rays);
 }
 
-template <bool kBvh, int kNS>
+template <int kAcc, int kNS>
 __global__ __launch_bounds__(kWfBlock) void wf_shade(const WfArgs w, int it) {
     extern __shared__ float4 smem[];
-    const SceneView sc = wf_scene<kBvh>(w.a, w.lds != 0, w.bstk_off, smem, threadIdx.x);
+    const SceneView sc = wf_scene<kAcc>(w.a, w.lds != 0, w.bstk_off, smem, threadIdx.x);
     const int B = gridDim.x, j = blockIdx.x;
     const unsigned int nL = w.cnt[(size_t)(4 * it + 1) * B + j], nM = w.cnt[(size_t)(4 * it + 2) * B + j],
                        nD = w.cnt[(size_t)(4 * it + 3) * B + j];
@@ -267,7 +267,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade(const WfArgs w, int it) {
                 DeferredLight dl;
                 dl.on = false;
                 int nr = 0;
-                const F3 X = ScatterDir<kBvh, kNS>(mat, id, r, rec, lightE, nr, rng, sc, kBvh ? nullptr : &dl);
+                const F3 X = ScatterDir<kAcc, kNS>(mat, id, r, rec, lightE, nr, rng, sc, kAcc ? nullptr : &dl);
                 rays += (unsigned long long)nr;
                 w.rng[p] = rng;
                 const F3 dir = renormalize(normalize(X), sc.rnlut);

@@ -21,7 +21,9 @@ pytestmark = pytest.mark.gpu
 
 NO_BVH = 32
 V0, POOL = 2, 512   # LRT_F_SIMPLE (trace_kernel), LRT_F_POOL (pool_kernel)
-KERNELS = pytest.mark.parametrize("kflags", [V0, POOL], ids=["v0", "pool"])
+BVH, GRID = 1024, 2048   # LRT_F_BVH, LRT_F_GRID: the closest-hit structure (the grid is the default here)
+KERNELS = pytest.mark.parametrize("kflags", [V0, POOL, V0 | BVH, POOL | BVH],
+                                  ids=["v0-grid", "pool-grid", "v0-bvh", "pool-bvh"])
 
 
 def _bitwise(got, want, what):
@@ -52,9 +54,10 @@ def _render(gpu, flags=0, **kw):
 
 def _assert_instance(info, kflags, frames, samp="0"):
     """The instance the benchmark runs for this geometry: trace_kernel with 16 frame lanes
-    per pixel (v0), or pool_kernel with its tile size for `frames`."""
-    assert info["bvh"] == "1" and info["maxd"] == "8", info
-    if kflags == POOL:
+    per pixel (v0), or pool_kernel with its tile size for `frames`; through the uniform grid
+    (the library's pick for random_scene(1000)) or, with LRT_F_BVH, the BVH."""
+    assert info["acc"] == ("bvh" if kflags & BVH else "grid") and info["maxd"] == "8", info
+    if kflags & POOL:
         assert info["kernel"] == "pool_kernel" and info["pix"] == str(64 if frames <= 64 else 16), info
     else:
         assert info["kernel"] == "trace_kernel" and info["split"] == "16" and info["samp"] == samp, info
@@ -84,7 +87,7 @@ def test_config4_window_vs_oracle_and_linear_scan(gpu, scene1000, kflags):
     _bitwise(a, want, "config4 window vs oracle")
     assert ra == wr
     b, rb, info_b = _render(gpu, flags=NO_BVH | kflags, **kw)
-    assert info_b["bvh"] == "0" and info_b["kernel"] == info["kernel"]
+    assert info_b["acc"] == "scan" and info_b["kernel"] == info["kernel"]
     assert rb == ra and np.array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
@@ -93,7 +96,7 @@ def test_config4_many_tiles_bvh_equals_linear_scan(gpu, scene1000, kflags):
     """Enough 64-spp tiles that the persistent grid refills from its queues several times
     (every block runs many tasks): BVH == linear scan, rays included."""
     # pool tiles are 8x8 pixels at 64 spp: a larger window for more tiles than blocks
-    xc, yc = (768, 96) if kflags == V0 else (1536, 192)
+    xc, yc = (768, 96) if not kflags & POOL else (1536, 192)
     kw = dict(width=3840, height=2160, frames=64, max_depth=8, x0=1536, x_count=xc, y0=900, row_count=yc)
     a, ra, info = _render(gpu, flags=kflags, **kw)
     _assert_instance(info, kflags, 64)
@@ -141,20 +144,22 @@ def test_pool_tile_order_keeps_every_pixel(gpu, request, scene):
 
 
 
-def test_probe_ordered_first_launch_vs_oracle(gpu, scene1000):
+@pytest.mark.parametrize("acc", [0, BVH], ids=["grid", "bvh"])
+def test_probe_ordered_first_launch_vs_oracle(gpu, scene1000, acc):
     """A render signature whose geometry has no measured order yet runs its first (recording)
     launch in the order of the tile-cost probe (probe_kernel + probe_order_kernel, order=4;
-    the BVH probe here, the 9-sphere one in test_gpu_multidev). The probe only permutes the
-    tiles: pixels and ray count equal the restatement's. No other test uses the window's
-    shape, so no order can be borrowed."""
+    the grid's and the BVH's probe here, the 9-sphere one in test_gpu_multidev). The probe only
+    permutes the tiles: pixels and ray count equal the restatement's. No other test uses the
+    window's shape, so no order can be borrowed."""
     s, m = scene1000
-    kw = dict(width=3840, height=2160, frames=64, max_depth=8, x0=1712, x_count=88, y0=1000, row_count=40)
-    want, wr = oracle.orc_render(3840, 2160, 64, 8, 0, 1712, 88, 1000, 40, spheres=s, mats=m, threads=16)
-    buf, rays, info = _render(gpu, flags=POOL, **kw)
-    assert info["kernel"] == "pool_kernel" and info["bvh"] == "1" and info["order"] == "4", info
+    x0 = 1712 if acc else 1616   # a window per structure: each one's first launch probes
+    kw = dict(width=3840, height=2160, frames=64, max_depth=8, x0=x0, x_count=88, y0=1000, row_count=40)
+    want, wr = oracle.orc_render(3840, 2160, 64, 8, 0, x0, 88, 1000, 40, spheres=s, mats=m, threads=16)
+    buf, rays, info = _render(gpu, flags=POOL | acc, **kw)
+    assert info["kernel"] == "pool_kernel" and info["acc"] == ("bvh" if acc else "grid") and info["order"] == "4", info
     _bitwise(buf, want, "probe-ordered first launch")
     assert rays == wr
-    buf2, rays2, info2 = _render(gpu, flags=POOL, **kw)   # then the measured order
+    buf2, rays2, info2 = _render(gpu, flags=POOL | acc, **kw)   # then the measured order
     assert info2["order"] == "2", info2
     _bitwise(buf2, want, "measured order")
     assert rays2 == wr
