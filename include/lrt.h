@@ -182,6 +182,10 @@ int lrt_camera_default(int width, int height, lrt_camera* out);
  * 1 <= count <= LRT_MAX_SPHERES; material types must be 0..2. Emissive spheres are
  * those with any emissive channel > 0 (parallel.cpp:96). */
 int lrt_set_scene(const lrt_sphere* spheres, const lrt_material* materials, int count);
+/* The scene the devices hold (what lrt_set_scene last uploaded, or the default scene):
+ * *count spheres; copies them when capacity >= *count. */
+int lrt_get_scene(lrt_sphere* spheres, lrt_material* materials, int capacity, int* count);
+
 /* Copy the reference's default scene (9 spheres) into caller arrays of >= 9 entries. */
 int lrt_default_scene(lrt_sphere* spheres, lrt_material* materials, int capacity, int* count);
 

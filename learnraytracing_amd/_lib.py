@@ -110,6 +110,7 @@ SIGNATURES = {
     "lrt_camera_default": (_i, [_i, _i, _c.POINTER(Camera)]),
     "lrt_set_scene": (_i, [_c.POINTER(Sphere), _c.POINTER(Material), _i]),
     "lrt_default_scene": (_i, [_c.POINTER(Sphere), _c.POINTER(Material), _i, _c.POINTER(_i)]),
+    "lrt_get_scene": (_i, [_c.POINTER(Sphere), _c.POINTER(Material), _i, _c.POINTER(_i)]),
     "lrt_render_device": (_i, [_c.POINTER(RenderDesc), _vp, _vp, _vp]),
     "lrt_render_device_to_frame": (_i, [_c.POINTER(RenderDesc), _vp, _vp, _vp, _vp]),
     "lrt_ipc_alloc": (_i, [_c.c_size_t, _c.POINTER(_vp), _vp]),

@@ -190,6 +190,17 @@ int lrt_set_scene(const lrt_sphere* spheres, const lrt_material* materials, int 
     return LRT_OK;
 }
 
+int lrt_get_scene(lrt_sphere* spheres, lrt_material* materials, int capacity, int* count) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!ctx().ready) return fail(LRT_E_STATE, "lrt_initialize() has not been called");
+    const int n = (int)ctx().spheres.size();
+    if (count) *count = n;
+    if (!spheres || !materials || capacity < n) return fail(LRT_E_INVALID, "need capacity >= the scene's sphere count");
+    memcpy(spheres, ctx().spheres.data(), sizeof(lrt_sphere) * n);
+    memcpy(materials, ctx().mats.data(), sizeof(lrt_material) * n);
+    return LRT_OK;
+}
+
 int lrt_default_scene(lrt_sphere* spheres, lrt_material* materials, int capacity, int* count) {
     if (count) *count = 9;
     if (capacity < 9 || !spheres || !materials) return fail(LRT_E_INVALID, "need capacity >= 9");

@@ -16,9 +16,9 @@
 // every ray point up to that exit lies within the DDA's rounding error of a visited cell, a
 // sphere's hit point lies in its box, and the box was padded by more than that error -- so a
 // sphere not yet tested has cand > the exit >= best and can neither win nor tie. Rays whose
-// rounding bound (from |origin| and the entry distance) exceeds the padding's share scan every
-// sphere instead (never in practice). No stack: the walk's state is a cell and three plane
-// times, so the traversal holds fewer registers than the BVH's and no LDS.
+// rounding bound (from |origin| and the box's extent) exceeds the padding's share scan every
+// sphere instead (origins more than ~8 scene sizes away). No stack: the walk's state is a
+// cell and three plane times, so the traversal holds fewer registers than the BVH's and no LDS.
 //
 // Walk and sphere tests share ONE loop (GridStep): an iteration advances to the next cell
 // when the current cell's list is used up, then tests one sphere. A wave therefore runs max
@@ -40,7 +40,7 @@ struct GridView {
     float hx, hy, hz;        // cell size per axis
     float ihx, ihy, ihz;     // 1 / cell size
     float pad;               // insertion padding (absolute)
-    float errk;              // a ray may walk if 2^-18 (max|o| + tEnter + ext) < errk (= pad / 2)
+    float errk;              // a ray may walk if 2^-16 (max|o| + ext) < errk (= pad / 2)
     float ext;               // max |coordinate| of the box
     int on;
 };
@@ -92,6 +92,18 @@ LRT_DEV void GridStart(GridQuery& q, const GridView& g, GridStats* st = nullptr)
     q.inv = f3(rcp_rn(q.d.x), rcp_rn(q.d.y), rcp_rn(q.d.z));
     q.mode = 2;
     if (g.count == 0 || g.nx == 0) return;
+    // The walk's rounding bound, 2^-18 (max|o| + tEnter + ext) <= 2^-16 (max|o| + ext) (tEnter is
+    // at most sqrt(3) (max|o| + ext)), must stay below errk; else (a huge origin, NaN) scan every
+    // sphere. Decided before the box test: that test's own rounding grows with |o| too.
+    const float mo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(q.o.x), __builtin_fabsf(q.o.y)),
+                                     __builtin_fabsf(q.o.z));
+    if (!((mo + g.ext) * 1.52587890625e-05f < g.errk)) {
+        if (st) st->fallback += 1;
+        q.mode = 1;
+        q.j = 0;
+        q.jend = (unsigned)g.count;
+        return;
+    }
     const float hix = GridPlane(g.lox, g.nx, g.hx), hiy = GridPlane(g.loy, g.ny, g.hy),
                 hiz = GridPlane(g.loz, g.nz, g.hz);
     // the box's slab interval; an axis the ray does not move along constrains through o
@@ -108,18 +120,8 @@ LRT_DEV void GridStart(GridQuery& q, const GridView& g, GridStats* st = nullptr)
     slab(q.o.x, q.d.x, q.inv.x, g.lox, hix);
     slab(q.o.y, q.d.y, q.inv.y, g.loy, hiy);
     slab(q.o.z, q.d.z, q.inv.z, g.loz, hiz);
-    // (a NaN from a huge origin fails every compare below: the fallback scan takes it)
     const float slack = g.pad + 1e-5f * t1;
     if (t0 > t1 + slack || q.bestT < t0 - g.pad - 1e-5f * t0) return;   // misses the box, or beaten before it
-    const float mo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(q.o.x), __builtin_fabsf(q.o.y)),
-                                     __builtin_fabsf(q.o.z));
-    if (!((mo + t0 + g.ext) * 3.814697265625e-06f < g.errk)) {   // 2^-18: the walk's rounding bound
-        if (st) st->fallback += 1;
-        q.mode = 1;
-        q.j = 0;
-        q.jend = (unsigned)g.count;
-        return;
-    }
     const F3 p = q.o + q.d * t0;
     auto cell = [](float p, float lo, float ih, int n) {
         const float f = (p - lo) * ih;

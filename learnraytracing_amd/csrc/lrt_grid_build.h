@@ -136,9 +136,9 @@ inline void build_grid_host(const lrt_sphere* s, int n, const std::vector<float4
         ext = std::max(ext, std::max(std::fabs(lo[k]), std::fabs(hi[k])));
         span = std::max(span, hi[k] - lo[k]);
     }
-    // padding: far above the walk's rounding (2^-18 (|o| + t + ext) with |o| + t up to ~40 x
-    // the scene's size), far below a cell
-    const float pad0 = 1e-5f * ext + 1e-4f * span + 1e-6f;
+    // padding: far above the walk's rounding (2^-16 (|o| + ext) for origins up to ~8 scene
+    // sizes away, lrt_grid.h), far below a cell (~1/40 of the span)
+    const float pad0 = 1e-5f * ext + 2.5e-4f * span + 1e-6f;
     float e3[3];
     double vol = 1.0;
     for (int k = 0; k < 3; ++k) {

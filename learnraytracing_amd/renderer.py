@@ -124,6 +124,18 @@ def set_scene(spheres: Sequence[L.Sphere], materials: Sequence[L.Material]) -> N
     L.check(L.lib().lrt_set_scene(sa, ma, n))
 
 
+def get_scene():
+    """(spheres, materials) the devices hold now (lrt_get_scene)."""
+    n = ctypes.c_int(0)
+    rc = L.lib().lrt_get_scene(None, None, 0, ctypes.byref(n))
+    if rc != 0 and n.value == 0:
+        L.check(rc)
+    sa = (L.Sphere * max(n.value, 1))()
+    ma = (L.Material * max(n.value, 1))()
+    L.check(L.lib().lrt_get_scene(sa, ma, n.value, ctypes.byref(n)))
+    return list(sa)[: n.value], list(ma)[: n.value]
+
+
 def shard_rows(height: int, row_block: int, period: int, phase: int) -> int:
     return L.check(L.lib().lrt_shard_rows(int(height), int(row_block), int(period), int(phase)))
 

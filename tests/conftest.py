@@ -43,3 +43,24 @@ def gpu():
     lrt.InitializeTest()
     yield lrt
     lrt.ShutdownTest()
+
+
+def _scene_bytes(scene):
+    sph, mat = scene
+    return b"".join(bytes(x) for x in sph) + b"".join(bytes(x) for x in mat)
+
+
+@pytest.fixture(autouse=True)
+def _scene_guard(request):
+    """GPU tests start on the reference's default scene (parallel.cpp:15-51). A test that
+    changes the scene restores it (try/finally, or a function-scoped scene fixture); one that
+    does not would hand its scene to whatever test runs next -- the r3_ae red run, where a
+    9-sphere oracle comparison rendered a module fixture's 1000-sphere scene -- so the leak is
+    reported here, loudly, at the next test's start."""
+    if "gpu" in request.keywords and "gpu" in request.fixturenames:
+        import learnraytracing_amd as lrt
+        if lrt.lib().lrt_device_count() > 0 and _scene_bytes(lrt.get_scene()) != _scene_bytes(lrt.default_scene()):
+            lrt.set_scene(*lrt.default_scene())
+            pytest.fail("the library held a non-default scene at this test's start: an earlier test leaked it "
+                        "(it was reset to the default scene)")
+    yield

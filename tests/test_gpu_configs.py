@@ -35,13 +35,22 @@ def _bitwise(got, want, what):
 
 
 @pytest.fixture(scope="module")
-def scene1000(gpu):
-    from learnraytracing_amd.scene import scene_arrays
-    sph, mat = gpu.random_scene(1000, 1)
+def _scene1000_arrays():
+    from learnraytracing_amd.scene import random_scene, scene_arrays
+    sph, mat = random_scene(1000, 1)
+    return (sph, mat), tuple(np.array(v, np.float32) for v in scene_arrays(sph, mat))
+
+
+@pytest.fixture
+def scene1000(gpu, _scene1000_arrays):
+    """random_scene(1000, 1) on the devices for one test, then the default scene again (the
+    scene guard in conftest.py checks that every GPU test starts on the default scene)."""
+    (sph, mat), arrays = _scene1000_arrays
     gpu.set_scene(sph, mat)
-    s, m = (np.array(v, np.float32) for v in scene_arrays(sph, mat))
-    yield s, m
-    gpu.set_scene(*gpu.default_scene())
+    try:
+        yield arrays
+    finally:
+        gpu.set_scene(*gpu.default_scene())
 
 
 def _render(gpu, flags=0, **kw):
