@@ -134,13 +134,15 @@ def cpu_baseline(cfg, budget_s: float, cores: int):
 def drawtest_leg(lrt, frames: int = 200):
     """lrt_draw_test as src/cpu/main.cpp drives DrawTest: one pageable `new float[]` backbuffer
     (main.cpp:40) handed to every frame (main.cpp:165) at 1280x720, kMaxDepth 20, frameCount
-    counting up. The first two frames (staged, then the registration cache page-locks the
-    buffer) are untimed; the rate is rays / wall time over the next `frames` frames, the same
-    unit as cpu_reference_drawtest (the reference's DrawTest on the host cores)."""
+    counting up. Each call page-locks the buffer for itself only (nothing is kept between
+    calls). The first two frames are untimed; the rate is rays / wall time over the next
+    `frames` frames, the same unit as cpu_reference_drawtest (the reference's DrawTest on the
+    host cores)."""
     import numpy as np
 
     from learnraytracing_amd import _lib as L
     w, h = 1280, 720
+    lrt.set_scene(*lrt.default_scene())   # DrawTest renders the reference's scene (parallel.cpp:15-51)
     bb = np.zeros(w * h * 4, np.float32)
     for f in range(2):
         lrt.DrawTest(0.0, f, w, h, bb)
@@ -150,7 +152,6 @@ def drawtest_leg(lrt, frames: int = 200):
         rays += lrt.DrawTest(0.0, f, w, h, bb)
     dt = time.perf_counter() - t0
     info = L.last_launch()
-    lrt.host_unregister(bb)
     return {"value": round(rays / dt / 1e6, 1), "unit": "Mray/s", "ms_per_frame": round(dt / frames * 1e3, 4),
             "frames": frames, "host_path": info.get("host"), "lookahead": info.get("lookahead"),
             "what": "lrt_draw_test(0, f, 1280, 720, pageable backbuffer) per frame, host wall clock (H2D of the "
@@ -175,8 +176,11 @@ def cpu_reference_drawtest(cores: int, budget_s: float):
 
 def scene_reads(info: dict) -> str:
     """Where the launched instance reads the scene from, taken from lrt_last_launch()'s
-    lds= / bvh= words (not from the flags asked for)."""
+    lds= / acc= words (not from the flags asked for)."""
     lds, bvh = info.get("lds"), info.get("bvh")
+    if info.get("acc") == "grid":
+        return ("uniform grid: cell lists + cell-ordered spheres through L1/L2 (global memory), materials "
+                + ("LDS-staged" if lds == "1" else "through L1/L2"))
     if bvh == "1":
         return ("BVH nodes + leaf spheres through L1/L2 (global memory), materials "
                 + ("LDS-staged" if lds == "1" else "through L1/L2"))

@@ -128,7 +128,6 @@ int lrt_device_count(void) {
 int lrt_shutdown(void) {
     std::lock_guard<std::mutex> lk(g_mu);
     if (g_ndev == 0) return LRT_OK;
-    host_release_all();
     if (g_multi.rccl)
         for (int k = 0; k < g_ndev; ++k) (void)ncclCommDestroy(g_multi.comms[k]);
     for (int k = 0; k < g_ndev; ++k) {

@@ -51,14 +51,12 @@ inline void build_grid_host(const lrt_sphere* s, int n, const std::vector<float4
         big_r = 8.0f * fin[m];
     }
     std::vector<char> big(n, 0);
-    int nbig = 0;
     std::vector<int> in;
     for (int i = 0; i < n; ++i) {
         const bool finite = std::isfinite(s[i].center.x) && std::isfinite(s[i].center.y) &&
                             std::isfinite(s[i].center.z) && std::isfinite(radii[i]);
         if (!finite || radii[i] > big_r) {
             big[i] = 1;
-            ++nbig;
         } else {
             in.push_back(i);
         }
@@ -118,7 +116,6 @@ inline void build_grid_host(const lrt_sphere* s, int n, const std::vector<float4
             }
         if (bestj < 0 || bestv > v0 * (2.0 / 3.0)) break;
         big[in[bestj]] = 1;
-        ++nbig;
         in.erase(in.begin() + bestj);
     }
     for (int i = 0; i < n; ++i)

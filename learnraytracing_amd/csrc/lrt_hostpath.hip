@@ -47,27 +47,17 @@ float* host_pinned(float* buf) {
     return at.devicePointer ? (float*)at.devicePointer : buf;
 }
 
-// Registration cache for pageable DrawTest buffers. The reference's caller allocates its
-// backbuffer with `new float[]` once (main.cpp:40) and hands the same pointer to every
-// DrawTest (main.cpp:165); pageable memory can only be staged (H2D + render + D2H: 0.77 ms
-// per 1280x720 frame). A pageable buffer seen by two consecutive lrt_draw_test
-// calls is page-locked in place (hipHostRegister, portable to every device in use) and from
-// then on takes the page-locked paths (pipelined DMA + lerp written over PCIe: 0.52 ms).
-// A registered range must not be freed while registered -- the GPU would later address
-// pages the process no longer maps -- so the contract is DrawTest's own (one buffer for the
-// run): lrt_host_unregister drops one before the caller frees it (the Python binding does it
-// when the array dies), lrt_shutdown drops all, at most kHostRegs stay registered (least
-// recently used dropped first). lrt_render_host never registers. LRT_HOST_REGISTER=0: off.
-struct HostReg {
-    void* p = nullptr;
-    size_t bytes = 0;
-    unsigned long long tick = 0;
-};
-constexpr int kHostRegs = 8;
-HostReg g_host_regs[kHostRegs];
-unsigned long long g_host_reg_tick = 0;
-HostReg g_host_last;   // the last pageable buffer rendered (registered when seen again)
-
+// A pageable backbuffer is page-locked for the duration of ONE call (HostLock): registered
+// when the call starts, unregistered before it returns, after every copy and kernel that
+// touches it has completed. The reference's caller owns its buffer across calls and may free
+// it and allocate another -- even at the same address -- between any two calls (parallel.h:8
+// has no unregister hook), so the library keeps no registration, no pointer and no pages
+// from one call to the next. Registering the 14.7 MB of a 1280x720 frame costs microseconds
+// (profiles/r4_b: tools/hostreg_probe.hip, which also remaps the same address between calls
+// and checks the device reads and writes the new pages), and turns the call's copies into
+// true DMA and its lerp into posted PCIe writes (the page-locked paths below) instead of the
+// runtime's bounce buffers (staged: 0.77 ms per frame). A buffer the caller page-locked
+// itself is used as it is. LRT_HOST_REGISTER=0: pageable buffers stay staged.
 bool host_register_on() {
     static const bool on = [] {
         const char* e = getenv("LRT_HOST_REGISTER");
@@ -76,43 +66,35 @@ bool host_register_on() {
     return on;
 }
 
-int host_unregister(void* p) {
-    for (auto& r : g_host_regs)
-        if (r.p == p) {
-            const hipError_t e = hipHostUnregister(r.p);
-            r = HostReg();
-            if (e != hipSuccess) return hip_fail(e, "hipHostUnregister");
-            return LRT_OK;
+struct HostLock {
+    void* p = nullptr;   // registered by this call (nullptr: nothing to undo)
+    float* dev = nullptr;
+    // the device address of buf's page-locked pages for this call, or nullptr (staged path)
+    float* acquire(float* buf, size_t bytes) {
+        if (!host_register_on()) return nullptr;
+        if (hipHostRegister(buf, bytes, hipHostRegisterPortable | hipHostRegisterMapped) != hipSuccess) {
+            (void)hipGetLastError();   // e.g. part of the range is registered already: stay staged
+            return nullptr;
         }
-    return fail(LRT_E_INVALID, "not a buffer the library registered");
-}
-
-bool host_registered_here(const void* p) {
-    for (const auto& r : g_host_regs)
-        if (r.p == p) return true;
-    return false;
-}
-
-// The device address of pageable buf once it is registered (see above), else nullptr.
-float* host_register(float* buf, size_t bytes) {
-    if (!host_register_on()) return nullptr;
-    const bool again = g_host_last.p == buf && g_host_last.bytes == bytes;
-    g_host_last.p = buf;
-    g_host_last.bytes = bytes;
-    if (!again) return nullptr;
-    HostReg* slot = &g_host_regs[0];
-    for (auto& r : g_host_regs)
-        if (r.tick < slot->tick) slot = &r;
-    if (slot->p) (void)host_unregister(slot->p);
-    if (hipHostRegister(buf, bytes, hipHostRegisterPortable | hipHostRegisterMapped) != hipSuccess) {
-        (void)hipGetLastError();   // e.g. overlaps a registered range: stay on the staged path
-        return nullptr;
+        p = buf;
+        dev = host_pinned(buf);
+        if (!dev) release();
+        return dev;
     }
-    slot->p = buf;
-    slot->bytes = bytes;
-    slot->tick = ++g_host_reg_tick;
-    return host_pinned(buf);
-}
+    // Unregisters once nothing in flight can touch the pages: the call's copies and lerps run on
+    // the context's stream and copy stream (idle by now on the normal path; on an error path
+    // this waits for what was enqueued). The look-ahead stream never touches them.
+    int release() {
+        if (!p) return LRT_OK;
+        (void)hipStreamSynchronize(ctx().stream);
+        if (ctx().s_in) (void)hipStreamSynchronize(ctx().s_in);
+        const hipError_t e = hipHostUnregister(p);
+        p = nullptr;
+        dev = nullptr;
+        return e == hipSuccess ? LRT_OK : hip_fail(e, "hipHostUnregister");
+    }
+    ~HostLock() { (void)release(); }
+};
 
 // Page-locked host backbuffers are rendered in place (zero copy): the kernel's 16 B read
 // and 16 B write per pixel cross PCIe inside the launch instead of a staging copy either
@@ -308,10 +290,10 @@ int render_host_pipelined(const lrt_render_desc* d, float* buf, float* hdev, siz
     return LRT_OK;
 }
 
-// allow_register: the reference API's call (lrt_draw_test), whose caller keeps one buffer for
-// the whole run (main.cpp:40,165): a pageable buffer may be page-locked (host_register).
+// drawtest: the reference API's call (lrt_draw_test), whose caller asks for frameCount + 1 next
+// (main.cpp:165,187): the pipelined path renders that frame's colours ahead (the look-ahead).
 int render_host(const lrt_render_desc* d, float* buf, long long* out_rays, const lrt_features* feat,
-                bool allow_register) {
+                bool drawtest) {
     int rc = validate(d);
     if (rc) return rc;
     if (!ctx().ready) return fail(LRT_E_STATE, "lrt_initialize() has not been called");
@@ -325,18 +307,18 @@ int render_host(const lrt_render_desc* d, float* buf, long long* out_rays, const
     // contiguous rows; a caller's own row-block-cyclic shard, or features, stay on device 0)
     if (g_multi.on && d->row_period == 1 && !feat) return render_host_multi(d, buf, bytes, out_rays);
     // lrt_last_launch() names the host path too: host=pipelined | zerocopy | staged, with
-    // "registered-" when the registration cache page-locked a pageable buffer
+    // "registered-" when this call page-locked a pageable buffer (HostLock)
     auto note = [](const char* path, bool registered) {
         const size_t n = strlen(g_last_launch);
         snprintf(g_last_launch + n, sizeof(g_last_launch) - n, " host=%s%s", registered ? "registered-" : "", path);
     };
     float* hdev = (!feat && host_zero_copy()) ? host_pinned(buf) : nullptr;
-    bool registered = hdev && host_registered_here(buf);
-    if (allow_register && !hdev && !feat && host_zero_copy()) registered = (hdev = host_register(buf, bytes)) != nullptr;
+    HostLock lock;   // a pageable buffer, page-locked for this call only
+    const bool registered = !hdev && !feat && host_zero_copy() && (hdev = lock.acquire(buf, bytes)) != nullptr;
     if (hdev && host_pipeline(d, bytes)) {
         if ((rc = ensure_frame(bytes))) return rc;
         int ahead = 0;
-        if ((rc = render_host_pipelined(d, buf, hdev, bytes, out_rays, allow_register, &ahead))) return rc;
+        if ((rc = render_host_pipelined(d, buf, hdev, bytes, out_rays, drawtest, &ahead))) return rc;
         note("pipelined", registered);
         const size_t m = strlen(g_last_launch);
         snprintf(g_last_launch + m, sizeof(g_last_launch) - m, " lookahead=%s", ahead ? "hit" : "miss");
@@ -391,12 +373,6 @@ int render_host(const lrt_render_desc* d, float* buf, long long* out_rays, const
     return LRT_OK;
 }
 
-void host_release_all() {
-    for (auto& r : g_host_regs)
-        if (r.p) (void)host_unregister(r.p);
-    g_host_last = HostReg();
-}
-
 }  // namespace lrt
 
 using namespace lrt;
@@ -404,10 +380,8 @@ using namespace lrt;
 extern "C" {
 
 int lrt_host_unregister(void* p) {
-    std::lock_guard<std::mutex> lk(g_mu);
-    if (!p) return LRT_OK;
-    if (g_host_last.p == p) g_host_last = HostReg();
-    return host_unregister(p);
+    (void)p;   // nothing to undo: a pageable buffer is page-locked only within a call (HostLock)
+    return LRT_OK;
 }
 
 }  // extern "C"

@@ -375,10 +375,9 @@ hipError_t fill_iota(int* v, int n, hipStream_t s);
 // ---- lrt_hostpath.hip
 int ensure_frame(size_t bytes);
 float* host_pinned(float* buf);
-// allow_register: the reference API's call (lrt_draw_test)
+// drawtest: the reference API's call (lrt_draw_test: the look-ahead render)
 int render_host(const lrt_render_desc* d, float* buf, long long* out_rays, const lrt_features* feat = nullptr,
-                bool allow_register = false);
-void host_release_all();   // lrt_shutdown: drops every registration the library made
+                bool drawtest = false);
 
 // ---- lrt_multi.hip
 int render_host_multi(const lrt_render_desc* d, float* buf, size_t bytes, long long* out_rays);

@@ -52,53 +52,21 @@ def device_count() -> int:
 
 
 def host_unregister(backbuffer: np.ndarray) -> None:
-    """Drop the library's page-locking of a pageable buffer it registered (DrawTest does this
-    by itself when the array is freed)."""
-    f = _registered.pop(backbuffer.ctypes.data, None)
-    if f is not None:
-        f.detach()
-    rc = L.lib().lrt_host_unregister(backbuffer.ctypes.data_as(ctypes.c_void_p))
-    if rc not in (L.LRT_OK, L.LRT_E_INVALID):
-        L.check(rc)
+    """No-op kept for callers of round 3's API: the library page-locks a pageable buffer only
+    for the duration of one call and keeps no registration between calls."""
+    L.check(L.lib().lrt_host_unregister(backbuffer.ctypes.data_as(ctypes.c_void_p)))
 
 
 def DrawTest(time: float, frameCount: int, screenWidth: int, screenHeight: int,
              backbuffer: np.ndarray) -> int:
+    """The reference's DrawTest (parallel.h:8): one progressive frame into the caller's
+    float RGBA backbuffer (any host memory; a pageable array is page-locked for the call
+    only). Returns the rays counted (outRayCount)."""
     _check_host_buffer(backbuffer, screenWidth * screenHeight * 4)
-    ptr = backbuffer.ctypes.data
     rays = ctypes.c_int(0)
     L.check(L.lib().lrt_draw_test(float(time), int(frameCount), int(screenWidth), int(screenHeight),
-                                  ctypes.c_void_p(ptr), ctypes.byref(rays)))
-    # (the launch string is parsed only until the buffer's registration is tracked: per-frame
-    # Python work delays the next call's DMA)
-    if ptr not in _registered and L.last_launch().get("host", "").startswith("registered"):
-        _unregister_when_freed(backbuffer)
+                                  backbuffer.ctypes.data_as(ctypes.c_void_p), ctypes.byref(rays)))
     return rays.value
-
-
-_registered = {}   # data pointer -> weakref.finalize of the array that owns the memory
-
-
-def _unregister_when_freed(arr: np.ndarray) -> None:
-    """The library page-locked this pageable buffer (lrt_draw_test's registration cache): drop
-    the registration before numpy frees the memory (a freed range must not stay registered)."""
-    import weakref
-    owner = arr
-    while isinstance(owner.base, np.ndarray):
-        owner = owner.base
-    ptr = arr.ctypes.data
-    f = _registered.get(ptr)
-    if f is not None and f.alive:
-        return
-    _registered[ptr] = weakref.finalize(owner, _unregister_ptr, ptr)
-
-
-def _unregister_ptr(ptr: int) -> None:
-    _registered.pop(ptr, None)
-    try:
-        L.lib().lrt_host_unregister(ctypes.c_void_p(ptr))   # LRT_E_INVALID if already dropped
-    except Exception:  # pragma: no cover - interpreter shutdown
-        pass
 
 
 # ---- extended API -----------------------------------------------------------------------

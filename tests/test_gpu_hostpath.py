@@ -2,8 +2,8 @@
 under each of their implementations, in fresh processes (the path switches are read once
 per process): the pipelined path for page-locked buffers (colours rendered while the
 previous values are copied in by DMA, chunked lerp written straight to the host pixels;
-1, 3 and 8 row chunks), zero copy (LRT_HOST_PIPELINE=0), and the staged path for pageable
-buffers. Every one must give the oracle's bits and ray counts over several progressive
+1, 3 and 8 row chunks), zero copy (LRT_HOST_PIPELINE=0), a pageable buffer (page-locked for
+each call only, then the pipelined path) and the staged path (LRT_HOST_REGISTER=0). Every one must give the oracle's bits and ray counts over several progressive
 frames, with the caller's alpha untouched."""
 import os
 import subprocess
@@ -46,8 +46,9 @@ print("ok")
     ({"LRT_HOST_CHUNKS": "8"}, True, 96, 61),
     ({"LRT_DRAW_LOOKAHEAD": "0"}, True, 200, 117),      # no look-ahead render of the next frame
     ({"LRT_HOST_PIPELINE": "0"}, True, 200, 117),        # zero copy
-    ({}, False, 200, 117),                               # pageable: staged
-], ids=["pipe2", "pipe1", "pipe3", "pipe8", "nolookahead", "zerocopy", "pageable"])
+    ({}, False, 200, 117),                               # pageable: page-locked per call, pipelined
+    ({"LRT_HOST_REGISTER": "0"}, False, 200, 117),       # pageable, staged
+], ids=["pipe2", "pipe1", "pipe3", "pipe8", "nolookahead", "zerocopy", "pageable", "staged"])
 def test_drawtest_host_paths(env, pinned, w, h):
     code = SCRIPT.format(root=ROOT, oracle=os.path.join(ROOT, "oracle"), w=w, h=h, pinned=pinned)
     p = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), capture_output=True, text=True,

@@ -130,27 +130,57 @@ def test_initialize_devices_validation(gpu):
     assert gpu.device_count() == 1
 
 
-def test_pageable_drawtest_buffer_is_registered(gpu):
-    """main.cpp's pattern: one pageable buffer for every frame. The first call stages it, the
-    second registers it (host=registered-pipelined) -- same bits as the oracle's frames."""
+def _mmap_frame(nbytes, at=None):
+    """An anonymous mapping as a float32 array (MAP_FIXED at `at` when given): the way a C
+    caller's large `new float[]` gets its pages, and the way freeing it and allocating another
+    can return the same address."""
+    import ctypes
+    import mmap as _m
+    libc = ctypes.CDLL(None, use_errno=True)
+    libc.mmap.restype = ctypes.c_void_p
+    libc.mmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long]
+    libc.munmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    flags = _m.MAP_PRIVATE | _m.MAP_ANONYMOUS | (0x10 if at is not None else 0)   # 0x10: MAP_FIXED
+    p = libc.mmap(at, nbytes, _m.PROT_READ | _m.PROT_WRITE, flags, -1, 0)
+    assert p not in (None, ctypes.c_void_p(-1).value), "mmap failed"
+    arr = np.ctypeslib.as_array((ctypes.c_float * (nbytes // 4)).from_address(p))
+    return p, arr, lambda: libc.munmap(p, nbytes)
+
+
+def test_drawtest_pageable_buffer_freed_and_remapped_at_same_address(gpu):
+    """The drop-in contract (parallel.h:8): DrawTest keeps nothing of the caller's buffer
+    between calls. Frames 0-1 go into pageable buffer A; the caller frees A and maps a new
+    buffer B at the SAME address (munmap + mmap MAP_FIXED) holding A's values, and frames 2-3
+    go into B: every frame equals the oracle's (a registration kept from A's calls would make
+    the device read and write A's stale pages instead of B's). Each call page-locks the buffer
+    for itself only (host=registered-pipelined) and both the remapped and a fresh buffer take
+    that path at once."""
     from learnraytracing_amd import _lib as L
     w, h = 320, 180
-    gpu.DrawTest(0.0, 0, 8, 8, np.zeros(8 * 8 * 4, np.float32))   # the cache's "last buffer" is another one
-    bb = np.zeros(w * h * 4, np.float32)
+    nbytes = w * h * 16
     want = np.zeros((h, w, 4), np.float32)
+    p, a, free_a = _mmap_frame(nbytes)
+    a[:] = 0.0
     paths = []
+    for f in range(2):
+        gpu.DrawTest(0.0, f, w, h, a)
+        paths.append(L.last_launch().get("host"))
+        oracle.orc_render(w, h, 1, 20, frame0=f, buf=want)
+    _bitwise(a.reshape(h, w, 4), want, "buffer A")
+    keep = a.copy()
+    free_a()
+    p2, b, free_b = _mmap_frame(nbytes, at=p)
     try:
-        for f in range(4):
-            gpu.DrawTest(0.0, f, w, h, bb)
+        assert p2 == p, "the kernel did not reuse the address"
+        b[:] = keep
+        for f in range(2, 4):
+            gpu.DrawTest(0.0, f, w, h, b)
             paths.append(L.last_launch().get("host"))
             oracle.orc_render(w, h, 1, 20, frame0=f, buf=want)
+        _bitwise(b.reshape(h, w, 4), want, "buffer B at A's address")
     finally:
-        gpu.host_unregister(bb)
-    assert paths[0] == "staged" and paths[1:] == ["registered-pipelined"] * 3, paths
-    _bitwise(bb.reshape(h, w, 4), want, "registered DrawTest")
-    # unregistered again: the next call stages (and a fresh buffer is not registered at once)
-    gpu.DrawTest(0.0, 4, w, h, bb)
-    assert L.last_launch()["host"] == "staged"
+        free_b()
+    assert paths == ["registered-pipelined"] * 4, paths
 
 
 def _torch_render(gpu, job, stream, out):
