@@ -307,20 +307,23 @@ def main():
     # remote exchange: rank 0's frames mapped into every rank; each render stores its finished
     # pixels there itself (no pack, gather or unshard launch per step)
     remote = world > 1 and args.exchange == "remote"
+    # with N > 1 both exchanges are timed (the other one as a second leg, unless
+    # --no-extra-legs): the fused remote stores, and north_star's RCCL gather over xGMI
+    both = world > 1 and extra
     shared = None
-    if remote:
+    if remote or both:
         dev_b = dev if backend == "nccl" else torch.device("cpu")
         shared = open_shared_frames(W, H, nslots, rank, dev_b)
         if shared is None:   # IPC mapping refused on some rank: the RCCL exchange instead
             log("note: IPC frame mapping failed on a rank; falling back to --exchange rccl")
             remote = False
-    gather_ex = world > 1 and not remote
+    have_rccl = world > 1 and (not remote or both)
     # the RCCL exchange carries RGB only (lrt_pack_rgb): 12 of the 16 bytes per pixel cross xGMI
-    packed = [torch.empty((max_rows, W, 3), dtype=torch.float32, device=dev) if gather_ex else None
+    packed = [torch.empty((max_rows, W, 3), dtype=torch.float32, device=dev) if have_rccl else None
               for _ in range(nslots)]
-    gathered = [torch.empty((world, max_rows, W, 3), dtype=torch.float32, device=dev) if rank == 0 and gather_ex
+    gathered = [torch.empty((world, max_rows, W, 3), dtype=torch.float32, device=dev) if rank == 0 and have_rccl
                 else None for _ in range(nslots)]
-    frames_out = [torch.empty((H, W, 4), dtype=torch.float32, device=dev) if rank == 0 and gather_ex else None
+    frames_out = [torch.empty((H, W, 4), dtype=torch.float32, device=dev) if rank == 0 and have_rccl else None
                   for _ in range(nslots)]
     stream = torch.cuda.current_stream(dev)
     # render streams (the first is the current stream); frame assembly and D2H on their own
@@ -328,12 +331,13 @@ def main():
     astream = torch.cuda.Stream(device=dev) if world > 1 else stream
     cstream = torch.cuda.Stream(device=dev)
     host = None   # pinned frame copies (end-to-end leg)
-    pending = []   # (work, slot, k) of steps whose gather / D2H is not yet enqueued
+    pending = []   # (mode, work, slot, d2h, rdone) of steps whose gather / D2H is not yet enqueued
 
-    def finish(work, slot, d2h, rdone):
+    def finish(mode, work, slot, d2h, rdone):
         """Assemble slot's frame on rank 0 (after its gather), then optionally copy it to
         pinned host memory; the slot's next render waits for both."""
         done = None
+        gather_ex = mode == "rccl"
         if gather_ex:
             done = torch.cuda.Event()
             with torch.cuda.stream(astream):
@@ -351,10 +355,12 @@ def main():
         if done is not None:
             rstreams[slot % nstreams].wait_event(done)
 
-    def step(k, d2h=False):
+    def step(k, mode, d2h=False):
+        """mode: "remote" (stores into rank 0's IPC frame), "rccl" (pack + gather + unshard), or
+        "local" (N = 1)."""
         slot = k % nslots
         rs = rstreams[k % nstreams]
-        if remote:
+        if mode == "remote":
             render_tensor_to_frame(job, bufs[slot], rays, shared.ptrs[slot], rs)
         else:
             lrt.render_tensor(job, bufs[slot], rays, rs)
@@ -363,13 +369,13 @@ def main():
             rdone = torch.cuda.Event()
             rdone.record(rs)
         work = None
-        if gather_ex:
+        if mode == "rccl":
             with torch.cuda.stream(rs):   # the gather is ordered after this step's render
                 pack_rgb_tensor(bufs[slot], packed[slot], rs)
                 _, work = gather_to_root(packed[slot], max_rows, world, rank, gathered=gathered[slot], async_op=True)
         while pending:
             finish(*pending.pop(0))
-        pending.append((work, slot, d2h, rdone))
+        pending.append((mode, work, slot, d2h, rdone))
 
     def drain():
         while pending:
@@ -385,23 +391,54 @@ def main():
     # at least one warmup step per render stream: a stream's first launch grows the
     # stream-ordered pool for its per-launch buffers (overflow stack, sample planes)
     warmup = max(args.warmup, nstreams)
-    for k in range(warmup):
-        step(k)
-    drain()
-    sync_all()
-    rays.zero_()
-    sync_all()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(warmup + k)
-    drain()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    if world > 1:
-        dist.barrier()
-    elapsed = t1 - t0
-    timed_rays = float(rays.item())
+
+    def timed(mode):
+        """warmup + K timed steps of `mode`: (seconds, counted rays of this rank)."""
+        for k in range(warmup):
+            step(k, mode)
+        drain()
+        sync_all()
+        rays.zero_()
+        sync_all()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            step(warmup + k, mode)
+        drain()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        if world > 1:
+            dist.barrier()
+        return t1 - t0, float(rays.item())
+
+    mode = ("remote" if remote else "rccl") if world > 1 else "local"
+    elapsed, timed_rays = timed(mode)
     launch_info = L.last_launch()
+    exchange_legs = None
+    if both and shared is not None:
+        # the other exchange, same steps; then both legs' assembled frames, bit for bit, on rank 0
+        other = "rccl" if mode == "remote" else "remote"
+        e2, r2 = timed(other)
+        legs = {mode: (elapsed, timed_rays), other: (e2, r2)}
+        st = torch.tensor([legs["remote"][0], legs["rccl"][0], legs["remote"][1], legs["rccl"][1]],
+                          dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        mx, sm = st.clone(), st.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        same = None
+        if rank == 0:
+            a, b = shared.tensor(0)[..., :3].contiguous(), frames_out[0][..., :3].contiguous()
+            same = bool(torch.equal(a.view(torch.int32), b.view(torch.int32)))
+        exchange_legs = {
+            "primary": mode,
+            "frames_identical": same,
+            "legs": {m: {"ms_per_step": round(float(mx[i]) / args.steps * 1e3, 4),
+                         "value": round(float(sm[2 + i]) / float(mx[i]) / 1e6, 3), "unit": "Mray/s",
+                         "what": ("each render stores its finished pixels into rank 0's frame over xGMI (IPC)"
+                                  if m == "remote" else
+                                  "pack to RGB + RCCL gather (dist.gather over nccl = RCCL) to rank 0 + unshard")}
+                     for i, m in enumerate(("remote", "rccl"))},
+        }
+    remote = mode == "remote"
 
     # ---- extra legs: each launch alone (roofline duration), end to end (D2H included)
     alone_ms = e2e_s = None
@@ -425,7 +462,7 @@ def main():
         e2e_steps = max(1, min(args.steps, 10))
         if remote:   # a frame is complete once every rank's render of it is: barrier, then D2H
             def e2e_step(k):
-                step(k)
+                step(k, mode)
                 sync_all()
                 if rank == 0:
                     host[k % nslots].copy_(shared.tensor(k % nslots))
@@ -439,20 +476,31 @@ def main():
             dist.barrier()
         else:
             for k in range(nslots):   # untimed: each pinned buffer's first copy maps its pages
-                step(k, d2h=True)
+                step(k, mode, d2h=True)
             drain()
             sync_all()
             t2 = time.perf_counter()
             for k in range(e2e_steps):
-                step(k, d2h=True)
+                step(k, mode, d2h=True)
             drain()
             torch.cuda.synchronize()
             e2e_s = time.perf_counter() - t2
             if world > 1:
                 dist.barrier()
 
-    # ---- the reference API as its own caller uses it (rank 0, N = 1): DrawTest per frame
+    # ---- the reference API as its own caller uses it (rank 0, N = 1): DrawTest per frame, on
+    # one device and split over two contexts of it (lrt_initialize_devices([0, 0]): the
+    # multi-device host path's own cost, rehearsed on the one GPU this process drives)
     drawtest = drawtest_leg(lrt) if extra and world == 1 else None
+    drawtest_multi = None
+    if extra and world == 1:
+        torch.cuda.synchronize()
+        lrt.ShutdownTest()
+        lrt.InitializeDevices([gpu, gpu])
+        drawtest_multi = drawtest_leg(lrt, frames=100)
+        drawtest_multi["devices"] = f"[{gpu}, {gpu}] (lrt_initialize_devices, direct exchange)"
+        lrt.ShutdownTest()
+        lrt.InitializeTest()
     torch.cuda.synchronize()
 
     stats = torch.tensor([elapsed, timed_rays, alone_ms or 0.0, e2e_s or 0.0], dtype=torch.float64,
@@ -570,6 +618,8 @@ def main():
             "cpu_baseline_1core": cpu1,
             "cpu_reference_drawtest": cpu_dt,
             "drawtest": drawtest,
+            "drawtest_multi": drawtest_multi,
+            "exchange": exchange_legs,
         }
         print(json.dumps(out), flush=True)
     if rstream is not None:

@@ -147,18 +147,26 @@ int lrt_draw_test(float time, int frameCount, int screenWidth, int screenHeight,
 /* ---- multi-GPU (one process) ---------------------------------------------- */
 
 /* InitializeTest over several devices (BASELINE config 5: the frame row-tiled across the
- * node's GPUs, assembled by an RCCL gather over xGMI). Instead of lrt_initialize: n device
- * ids (n = 0 and device_ids = NULL: every visible device). Afterwards lrt_draw_test and
- * lrt_render_host(_ex without features) split the caller's rows over all of them in blocks of
- * 8 rows dealt round-robin (row-block-cyclic; LRT_ROW_BLOCK overrides), each device renders its
- * rows with the previous values copied from the caller's buffer, and the shards are gathered
- * into the first device -- ncclCommInitAll + a grouped ncclGather (RCCL) when the ids are
+ * node's GPUs). Instead of lrt_initialize: n device ids (n = 0 and device_ids = NULL: every
+ * visible device). Afterwards lrt_draw_test and lrt_render_host(_ex without features) split
+ * the caller's rows over all of them in blocks of 8 rows dealt round-robin (row-block-cyclic;
+ * LRT_ROW_BLOCK overrides); each device copies its rows' previous values from the caller's
+ * buffer (page-locked for the call), renders them, and by default copies them straight back
+ * over its own PCIe link. With LRT_DEV_GATHER the shards' RGB is gathered into the first
+ * device instead -- ncclCommInitAll + a grouped ncclGather (RCCL, over xGMI) when the ids are
  * distinct, device-to-device copies when an id repeats (RCCL refuses two ranks on one GPU) or
  * with LRT_DEV_PEER_COPY -- which assembles the frame and copies it to the caller. The result
- * is bit-identical to one device. The other calls (lrt_render_device, streams, scene) act on
- * the first device; lrt_set_scene updates every device. lrt_shutdown releases all. */
-#define LRT_DEV_PEER_COPY 1 /* gather with device-to-device copies instead of RCCL */
+ * is bit-identical to one device either way. The other calls (lrt_render_device, streams,
+ * scene) act on the first device; lrt_set_scene updates every device. lrt_shutdown releases
+ * all. */
+#define LRT_DEV_PEER_COPY 1 /* gather, with device-to-device copies instead of RCCL */
+#define LRT_DEV_GATHER 2    /* gather the shards into the first device (RCCL when the ids are distinct) */
 int lrt_initialize_devices(int n, const int* device_ids, int flags);
+/* Bytes one multi-device host render of an x_count x rows window moves between the devices
+ * and the caller: *direct = the RGBA rows each device copies back over its own link (the
+ * default exchange); *gather_xgmi = the packed RGB (12 B per pixel) the other devices' shards
+ * send to the first one (LRT_DEV_GATHER). No device is touched. */
+int lrt_exchange_bytes(int x_count, int rows, int row_block, int devices, long long* direct, long long* gather_xgmi);
 /* Devices in use (0 before lrt_initialize / lrt_initialize_devices). */
 int lrt_device_count(void);
 

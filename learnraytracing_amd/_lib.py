@@ -35,6 +35,7 @@ F_V3 = 128          # removed in round 3: rejected with LRT_E_INVALID
 F_WAVEFRONT = 256
 F_POOL = 512
 DEV_PEER_COPY = 1   # lrt_initialize_devices: gather by device-to-device copies, not RCCL
+DEV_GATHER = 2      # lrt_initialize_devices: gather the shards into the first device (RCCL)
 IPC_HANDLE_BYTES = 64
 
 
@@ -124,6 +125,7 @@ SIGNATURES = {
     "lrt_stream_destroy": (_i, [_vp]),
     "lrt_host_alloc": (_i, [_c.c_size_t, _c.POINTER(_vp)]),
     "lrt_host_free": (_i, [_vp]),
+    "lrt_exchange_bytes": (_i, [_i, _i, _i, _i, _c.POINTER(_c.c_longlong), _c.POINTER(_c.c_longlong)]),
     "lrt_shard_rows": (_i, [_i, _i, _i, _i]),
     "lrt_unshard_rows": (_i, [_vp, _vp, _i, _i, _i, _i, _vp]),
     "lrt_pack_rgb": (_i, [_vp, _vp, _c.c_longlong, _vp]),

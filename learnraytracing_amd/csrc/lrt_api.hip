@@ -29,6 +29,7 @@ int init_context(Context& c, int dev) {
     c.device = dev;
     LRT_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
     LRT_HIP(hipMalloc(&c.d_rays, sizeof(unsigned long long)));
+    LRT_HIP(hipHostMalloc((void**)&c.h_rays, sizeof(unsigned long long), hipHostMallocDefault));
     LRT_HIP(hipMalloc(&c.d_tiles, sizeof(unsigned long long) * kQueueSlots * kTileSetU64));
     LRT_HIP(hipMemset(c.d_tiles, 0, sizeof(unsigned long long) * kQueueSlots * kTileSetU64));
     {   // parallel.cpp:262's lerpFac per frame number, divided once here instead of per wave
@@ -56,8 +57,9 @@ void free_context(Context& c) {
     if (c.stream) (void)hipStreamSynchronize(c.stream);
     (void)hipDeviceSynchronize();
     free_scene(c);
-    for (float* p : {c.d_frame, c.d_shard, c.d_gath})
+    for (float* p : {c.d_frame, c.d_shard, c.d_gath, c.d_pack})
         if (p) (void)hipFree(p);
+    if (c.h_rays) (void)hipHostFree(c.h_rays);
     if (c.d_rays) (void)hipFree(c.d_rays);
     if (c.d_tiles) (void)hipFree(c.d_tiles);
     if (c.d_lerp) (void)hipFree(c.d_lerp);

@@ -64,6 +64,18 @@ hipError_t launch_unshard(const float4* src, float4* dst, int width, int height,
     return hipGetLastError();
 }
 
+hipError_t launch_pack_rgb(const float4* src, float* dst, size_t n, hipStream_t s) {
+    pack_rgb_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(src, dst, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_unshard_rgb(const float* src, float4* dst, int width, int height, int rb, int period, int maxRows,
+                              hipStream_t s) {
+    dim3 grid((unsigned)((width + 255) / 256), (unsigned)height);
+    unshard_rgb_kernel<<<grid, 256, 0, s>>>(src, dst, width, height, rb, period, maxRows);
+    return hipGetLastError();
+}
+
 }  // namespace lrt
 
 using namespace lrt;

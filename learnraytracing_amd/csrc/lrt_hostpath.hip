@@ -303,9 +303,6 @@ int render_host(const lrt_render_desc* d, float* buf, long long* out_rays, const
         if (out_rays) *out_rays = 0;
         return LRT_OK;
     }
-    // lrt_initialize_devices: the caller's rows are split over every device (a window of
-    // contiguous rows; a caller's own row-block-cyclic shard, or features, stay on device 0)
-    if (g_multi.on && d->row_period == 1 && !feat) return render_host_multi(d, buf, bytes, out_rays);
     // lrt_last_launch() names the host path too: host=pipelined | zerocopy | staged, with
     // "registered-" when this call page-locked a pageable buffer (HostLock)
     auto note = [](const char* path, bool registered) {
@@ -315,6 +312,14 @@ int render_host(const lrt_render_desc* d, float* buf, long long* out_rays, const
     float* hdev = (!feat && host_zero_copy()) ? host_pinned(buf) : nullptr;
     HostLock lock;   // a pageable buffer, page-locked for this call only
     const bool registered = !hdev && !feat && host_zero_copy() && (hdev = lock.acquire(buf, bytes)) != nullptr;
+    // lrt_initialize_devices: the caller's rows are split over every device (a window of
+    // contiguous rows; a caller's own row-block-cyclic shard, or features, stay on device 0).
+    // render_host_multi returns with every device's stream idle, so the lock may go.
+    if (g_multi.on && d->row_period == 1 && !feat) {
+        rc = render_host_multi(d, buf, bytes, out_rays);
+        if (rc == LRT_OK) note(registered ? "registered-multi" : hdev ? "multi" : "pageable-multi", false);
+        return rc;
+    }
     if (hdev && host_pipeline(d, bytes)) {
         if ((rc = ensure_frame(bytes))) return rc;
         int ahead = 0;

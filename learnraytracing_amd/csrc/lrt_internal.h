@@ -246,6 +246,9 @@ struct Context {
     size_t shard_bytes = 0;
     float* d_gath = nullptr;
     size_t gath_bytes = 0;
+    float* d_pack = nullptr;   // the shard's RGB (the gather exchange)
+    size_t pack_bytes = 0;
+    unsigned long long* h_rays = nullptr;   // page-locked: the ray count's D2H stays asynchronous
     hipEvent_t ev_done = nullptr;   // this device's part of a multi-device render is enqueued
 };
 
@@ -261,7 +264,8 @@ inline Context& ctx() { return g_devs[g_cur]; }
 // Multi-device state (lrt_initialize_devices, lrt_multi.hip).
 struct Multi {
     bool on = false;          // host renders are split over the g_ndev contexts
-    bool rccl = false;        // the shards are gathered by RCCL (distinct devices); else peer copies
+    bool gather = false;      // the shards go to device 0 (LRT_DEV_GATHER / LRT_DEV_PEER_COPY); else direct
+    bool rccl = false;        // ... by RCCL (distinct devices); else peer copies
     int row_block = 8;        // rows per block of the row-block-cyclic split (LRT_ROW_BLOCK)
     ncclComm_t comms[kMaxDevices] = {};
 };
@@ -385,6 +389,9 @@ int render_host_multi(const lrt_render_desc* d, float* buf, size_t bytes, long l
 // ---- lrt_frame.hip
 hipError_t launch_unshard(const float4* src, float4* dst, int width, int height, int rb, int period, int maxRows,
                           hipStream_t s);
+hipError_t launch_pack_rgb(const float4* src, float* dst, size_t n, hipStream_t s);
+hipError_t launch_unshard_rgb(const float* src, float4* dst, int width, int height, int rb, int period, int maxRows,
+                              hipStream_t s);
 
 // ---- lrt_api.hip
 int init_context(Context& c, int dev);

@@ -21,53 +21,81 @@ int ensure_buffer(float*& p, size_t& have, size_t bytes, const char* what) {
 //   1. receives the previous values of its rows from the caller's buffer (one strided DMA),
 //   2. renders them densely into its shard buffer (lrt_render_desc's row map: row_period =
 //      N, row_phase = k; any kernel the policy picks),
-// then ONE collective brings the shards to device 0: a grouped ncclGather over RCCL
-// (rccl.h:745) when the devices are distinct, device-to-device copies when a device is
-// listed twice (RCCL refuses two ranks on one GPU: the 1-GPU rehearsal); device 0 assembles
-// the frame (unshard_kernel) and copies it to the caller. Per-pixel seeds make the frame
-// bit-identical to a 1-device render for any N and block size.
-int render_host_multi_enqueue(const lrt_render_desc* d, float* buf, size_t bytes, unsigned long long* rays);
+//   3. hands its rows back, by one of two exchanges:
+//      * direct (the default): its own strided DMA straight into the caller's rows, over
+//        its own PCIe link -- N links at once, no device in the middle;
+//      * gather (LRT_DEV_GATHER, or LRT_DEV_PEER_COPY): the RGB of its shard (12 of the 16 B
+//        per pixel: the render never writes alpha, parallel.cpp:283-285) to device 0 -- one
+//        grouped ncclGather over RCCL (rccl.h:745) when the devices are distinct, device-to-
+//        device copies when one is listed twice (RCCL refuses two ranks on one GPU) or with
+//        LRT_DEV_PEER_COPY -- where unshard_rgb_kernel assembles the frame over a copy of the
+//        caller's buffer (its alpha) and one DMA returns it.
+// The caller's buffer is page-locked for the call (render_host), so every copy is a real DMA
+// and every device's work is enqueued before the first blocking call: the devices overlap
+// (advisor r3: pageable copies ran synchronously, one device after the other). Per-pixel seeds
+// make the frame bit-identical to a 1-device render for any N, block size and exchange.
+int render_host_multi_enqueue(const lrt_render_desc* d, float* buf, size_t bytes);
 int render_host_multi(const lrt_render_desc* d, float* buf, size_t bytes, long long* out_rays) {
-    std::vector<unsigned long long> rays(g_ndev, 0ull);
-    const int rc = render_host_multi_enqueue(d, buf, bytes, rays.data());
+    const int rc = render_host_multi_enqueue(d, buf, bytes);
     long long total = 0;
-    for (int k = 0; k < g_ndev; ++k) {   // also after a failure: nothing may still write `rays`
+    for (int k = 0; k < g_ndev; ++k) {   // also after a failure: nothing may still write the counters
         DeviceScope ds(k);
         const hipError_t e = hipStreamSynchronize(ctx().stream);
         if (e != hipSuccess && rc == LRT_OK) return hip_fail(e, "hipStreamSynchronize(multi-device render)");
-        total += (long long)rays[k];
+        total += (long long)*ctx().h_rays;
     }
     if (rc) return rc;
     snprintf(g_last_launch + strlen(g_last_launch), sizeof(g_last_launch) - strlen(g_last_launch),
-             " devices=%d exchange=%s row_block=%d", g_ndev, g_multi.rccl ? "rccl" : "copy", g_multi.row_block);
+             " devices=%d exchange=%s row_block=%d", g_ndev,
+             !g_multi.gather ? "direct" : g_multi.rccl ? "rccl" : "copy", g_multi.row_block);
     if (out_rays) *out_rays = total;
     return LRT_OK;
 }
-int render_host_multi_enqueue(const lrt_render_desc* d, float* buf, size_t bytes, unsigned long long* rays) {
+
+// Bytes each exchange moves for an x_count x rows window over N devices (the CPU test of the
+// exchange's size): direct = every shard's RGBA rows back over its own link; gather = the
+// packed RGB of the shards into device 0 (the other devices' share crosses xGMI) plus the
+// frame's RGBA down from device 0.
+void multi_exchange_bytes(int xc, int rows, int b, int N, long long* direct, long long* gather_xgmi) {
+    const int maxRows = lrt_shard_rows(rows, b, N, 0);
+    *direct = (long long)xc * rows * 16;
+    *gather_xgmi = (long long)(N - 1) * maxRows * xc * 12;
+}
+
+int render_host_multi_enqueue(const lrt_render_desc* d, float* buf, size_t bytes) {
     const int N = g_ndev, b = g_multi.row_block, xc = d->x_count, rows = d->row_count;
     const size_t rowBytes = (size_t)xc * 16;
     const int maxRows = lrt_shard_rows(rows, b, N, 0);
     const size_t shardBytes = (size_t)maxRows * rowBytes;
+    const size_t packBytes = (size_t)maxRows * xc * 12;
+    const size_t blk = (size_t)b * rowBytes;
+    // shard row j is the caller's row (j / b) * b * N + k * b + j % b: whole blocks are one 2D
+    // copy (pitch N blocks), a last partial block one more -- in either direction
+    auto rows_copy = [&](int k, int rk, char* dev, hipMemcpyKind kind, hipStream_t s) -> hipError_t {
+        const int full = rk / b, tail = rk % b;
+        char* host = reinterpret_cast<char*>(buf) + (size_t)k * blk;
+        hipError_t e = hipSuccess;
+        if (full > 0)
+            e = kind == hipMemcpyHostToDevice
+                    ? hipMemcpy2DAsync(dev, blk, host, blk * N, blk, (size_t)full, kind, s)
+                    : hipMemcpy2DAsync(host, blk * N, dev, blk, blk, (size_t)full, kind, s);
+        if (e == hipSuccess && tail > 0)
+            e = kind == hipMemcpyHostToDevice
+                    ? hipMemcpyAsync(dev + (size_t)full * blk, host + (size_t)full * blk * N, (size_t)tail * rowBytes,
+                                     kind, s)
+                    : hipMemcpyAsync(host + (size_t)full * blk * N, dev + (size_t)full * blk, (size_t)tail * rowBytes,
+                                     kind, s);
+        return e;
+    };
     for (int k = 0; k < N; ++k) {
         DeviceScope ds(k);
         Context& c = ctx();
         if (int rc = ensure_buffer(c.d_shard, c.shard_bytes, shardBytes, "shard")) return rc;
+        if (g_multi.gather)
+            if (int rc = ensure_buffer(c.d_pack, c.pack_bytes, packBytes, "packed shard")) return rc;
         if (!c.ev_done) LRT_HIP(hipEventCreateWithFlags(&c.ev_done, hipEventDisableTiming));
         const int rk = lrt_shard_rows(rows, b, N, k);
-        if (rk > 0) {
-            // shard row j is the caller's row (j / b) * b * N + k * b + j % b: whole blocks
-            // are one 2D copy (pitch N blocks), a last partial block one more
-            const int full = rk / b, tail = rk % b;
-            const size_t blk = (size_t)b * rowBytes;
-            const char* src = reinterpret_cast<const char*>(buf) + (size_t)k * blk;
-            if (full > 0)
-                LRT_HIP(hipMemcpy2DAsync(c.d_shard, blk, src, blk * N, blk, (size_t)full, hipMemcpyHostToDevice,
-                                         c.stream));
-            if (tail > 0)
-                LRT_HIP(hipMemcpyAsync(reinterpret_cast<char*>(c.d_shard) + (size_t)full * blk,
-                                       src + (size_t)full * blk * N, (size_t)tail * rowBytes, hipMemcpyHostToDevice,
-                                       c.stream));
-        }
+        if (rk > 0) LRT_HIP(rows_copy(k, rk, reinterpret_cast<char*>(c.d_shard), hipMemcpyHostToDevice, c.stream));
         LRT_HIP(hipMemsetAsync(c.d_rays, 0, sizeof(unsigned long long), c.stream));
         lrt_render_desc sd = *d;
         sd.row_count = rk;
@@ -75,41 +103,46 @@ int render_host_multi_enqueue(const lrt_render_desc* d, float* buf, size_t bytes
         sd.row_period = N;
         sd.row_phase = k;
         if (int rc = render_device(&sd, c.d_shard, c.d_rays, nullptr, c.stream)) return rc;
-        LRT_HIP(hipMemcpyAsync(&rays[k], c.d_rays, sizeof(unsigned long long), hipMemcpyDeviceToHost, c.stream));
+        LRT_HIP(hipMemcpyAsync(c.h_rays, c.d_rays, sizeof(unsigned long long), hipMemcpyDeviceToHost, c.stream));
+        if (!g_multi.gather) {   // direct: this device's rows straight back to the caller
+            if (rk > 0) LRT_HIP(rows_copy(k, rk, reinterpret_cast<char*>(c.d_shard), hipMemcpyDeviceToHost, c.stream));
+            continue;
+        }
+        if (rk > 0)
+            LRT_HIP(launch_pack_rgb(reinterpret_cast<const float4*>(c.d_shard), c.d_pack, (size_t)rk * xc, c.stream));
         LRT_HIP(hipEventRecord(c.ev_done, c.stream));
     }
-    {   // the exchange: every shard into device 0's gather buffer
-        DeviceScope ds0(0);
-        Context& c0 = ctx();
-        if (int rc = ensure_buffer(c0.d_gath, c0.gath_bytes, shardBytes * N, "gather")) return rc;
-        if (int rc = ensure_frame(bytes)) return rc;
-        if (g_multi.rccl) {
-            const size_t count = shardBytes / sizeof(float);
-            if (ncclGroupStart() != ncclSuccess) return fail(LRT_E_HIP, "ncclGroupStart");
-            ncclResult_t r = ncclSuccess;
-            for (int k = 0; k < N && r == ncclSuccess; ++k) {
-                DeviceScope ds(k);
-                r = ncclGather(g_devs[k].d_shard, k == 0 ? c0.d_gath : nullptr, count, ncclFloat, 0, g_multi.comms[k],
-                               g_devs[k].stream);
-            }
-            const ncclResult_t r2 = ncclGroupEnd();
-            if (r != ncclSuccess || r2 != ncclSuccess)
-                return fail(LRT_E_HIP, std::string("ncclGather: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
-        } else {
-            for (int k = 0; k < N; ++k) {
-                LRT_HIP(hipStreamWaitEvent(c0.stream, g_devs[k].ev_done, 0));
-                char* dst = reinterpret_cast<char*>(c0.d_gath) + (size_t)k * shardBytes;
-                if (g_devs[k].device == c0.device)
-                    LRT_HIP(hipMemcpyAsync(dst, g_devs[k].d_shard, shardBytes, hipMemcpyDeviceToDevice, c0.stream));
-                else
-                    LRT_HIP(hipMemcpyPeerAsync(dst, c0.device, g_devs[k].d_shard, g_devs[k].device, shardBytes,
-                                               c0.stream));
-            }
+    if (!g_multi.gather) return LRT_OK;
+    // the gather: every packed shard into device 0, the frame assembled over the caller's values
+    DeviceScope ds0(0);
+    Context& c0 = ctx();
+    if (int rc = ensure_buffer(c0.d_gath, c0.gath_bytes, packBytes * N, "gather")) return rc;
+    if (int rc = ensure_frame(bytes)) return rc;
+    LRT_HIP(hipMemcpyAsync(c0.d_frame, buf, bytes, hipMemcpyHostToDevice, c0.stream));
+    if (g_multi.rccl) {
+        const size_t count = packBytes / sizeof(float);
+        if (ncclGroupStart() != ncclSuccess) return fail(LRT_E_HIP, "ncclGroupStart");
+        ncclResult_t r = ncclSuccess;
+        for (int k = 0; k < N && r == ncclSuccess; ++k) {
+            DeviceScope ds(k);
+            r = ncclGather(g_devs[k].d_pack, k == 0 ? c0.d_gath : nullptr, count, ncclFloat, 0, g_multi.comms[k],
+                           g_devs[k].stream);
         }
-        LRT_HIP(launch_unshard(reinterpret_cast<const float4*>(c0.d_gath), reinterpret_cast<float4*>(c0.d_frame), xc,
-                               rows, b, N, maxRows, c0.stream));
-        LRT_HIP(hipMemcpyAsync(buf, c0.d_frame, bytes, hipMemcpyDeviceToHost, c0.stream));
+        const ncclResult_t r2 = ncclGroupEnd();
+        if (r != ncclSuccess || r2 != ncclSuccess)
+            return fail(LRT_E_HIP, std::string("ncclGather: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+    } else {
+        for (int k = 0; k < N; ++k) {
+            LRT_HIP(hipStreamWaitEvent(c0.stream, g_devs[k].ev_done, 0));
+            char* dst = reinterpret_cast<char*>(c0.d_gath) + (size_t)k * packBytes;
+            if (g_devs[k].device == c0.device)
+                LRT_HIP(hipMemcpyAsync(dst, g_devs[k].d_pack, packBytes, hipMemcpyDeviceToDevice, c0.stream));
+            else
+                LRT_HIP(hipMemcpyPeerAsync(dst, c0.device, g_devs[k].d_pack, g_devs[k].device, packBytes, c0.stream));
+        }
     }
+    LRT_HIP(launch_unshard_rgb(c0.d_gath, reinterpret_cast<float4*>(c0.d_frame), xc, rows, b, N, maxRows, c0.stream));
+    LRT_HIP(hipMemcpyAsync(buf, c0.d_frame, bytes, hipMemcpyDeviceToHost, c0.stream));
     return LRT_OK;
 }
 
@@ -119,10 +152,18 @@ using namespace lrt;
 
 extern "C" {
 
+int lrt_exchange_bytes(int x_count, int rows, int row_block, int devices, long long* direct, long long* gather_xgmi) {
+    if (x_count < 0 || rows < 0 || row_block < 1 || devices < 1 || !direct || !gather_xgmi)
+        return fail(LRT_E_INVALID, "invalid exchange geometry");
+    multi_exchange_bytes(x_count, rows, row_block, devices, direct, gather_xgmi);
+    return LRT_OK;
+}
+
 int lrt_initialize_devices(int n, const int* device_ids, int flags) {
     std::lock_guard<std::mutex> lk(g_mu);
     if (g_ndev > 0) return fail(LRT_E_STATE, "already initialised: call lrt_shutdown() first");
-    if ((flags & ~LRT_DEV_PEER_COPY) != 0) return fail(LRT_E_INVALID, "unknown lrt_initialize_devices flags");
+    if ((flags & ~(LRT_DEV_PEER_COPY | LRT_DEV_GATHER)) != 0)
+        return fail(LRT_E_INVALID, "unknown lrt_initialize_devices flags");
     int visible = 0;
     LRT_HIP(hipGetDeviceCount(&visible));
     std::vector<int> ids;
@@ -154,13 +195,14 @@ int lrt_initialize_devices(int n, const int* device_ids, int flags) {
         for (int j = 0; j < i; ++j) distinct = distinct && ids[i] != ids[j];
     g_multi = Multi();
     if (const char* e = getenv("LRT_ROW_BLOCK")) g_multi.row_block = std::max(1, atoi(e));
-    if (rc == LRT_OK && distinct && !(flags & LRT_DEV_PEER_COPY)) {
+    g_multi.gather = (flags & (LRT_DEV_GATHER | LRT_DEV_PEER_COPY)) != 0;
+    if (rc == LRT_OK && g_multi.gather && distinct && !(flags & LRT_DEV_PEER_COPY)) {
         // one communicator per device, all in this process (the single-thread multi-device
         // form of RCCL); the gather is issued as a group (render_host_multi)
         const ncclResult_t r = ncclCommInitAll(g_multi.comms, N, ids.data());
         if (r != ncclSuccess) rc = fail(LRT_E_HIP, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
         g_multi.rccl = r == ncclSuccess;
-    } else if (rc == LRT_OK) {
+    } else if (rc == LRT_OK && g_multi.gather) {
         for (int i = 1; i < N; ++i)   // peer copies into device 0 (ignore "already enabled")
             if (ids[i] != ids[0]) {
                 (void)hipSetDevice(ids[0]);

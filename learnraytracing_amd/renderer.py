@@ -35,11 +35,13 @@ def ShutdownTest() -> None:
     L.check(L.lib().lrt_shutdown())
 
 
-def InitializeDevices(device_ids: Optional[Sequence[int]] = None, peer_copy: bool = False) -> None:
+def InitializeDevices(device_ids: Optional[Sequence[int]] = None, peer_copy: bool = False,
+                      gather: bool = False) -> None:
     """InitializeTest over several GPUs of this process (lrt_initialize_devices): DrawTest and
-    render_host then split the rows over all of them, gathered into the first by RCCL
+    render_host then split the rows over all of them; each device copies its rows back to the
+    caller's buffer itself, or with gather=True they are gathered into the first device by RCCL
     (device-to-device copies when an id repeats, or with peer_copy). None: every visible GPU."""
-    flags = L.DEV_PEER_COPY if peer_copy else 0
+    flags = (L.DEV_PEER_COPY if peer_copy else 0) | (L.DEV_GATHER if gather else 0)
     if device_ids is None:
         L.check(L.lib().lrt_initialize_devices(0, None, flags))
         return

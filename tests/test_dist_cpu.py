@@ -107,3 +107,19 @@ def test_shared_frames_failure_is_agreed(tmp_path, fail_rank):
         is_none, closed = np.load(tmp_path / f"r{r}.npy")
         assert bool(is_none) == (fail_rank >= 0)
         assert bool(closed) == (fail_rank >= 0 and r != fail_rank)
+
+
+def test_multidevice_exchange_bytes():
+    """lrt_exchange_bytes (no GPU): the direct exchange returns every pixel's RGBA once; the
+    gather sends the other devices' packed RGB (12 B per pixel) of the largest shard into the
+    first device. 1280x720 over 8 devices in row blocks of 8: shard 0 holds 12 blocks."""
+    import ctypes
+
+    from learnraytracing_amd import _lib as L
+    d, g = ctypes.c_longlong(0), ctypes.c_longlong(0)
+    L.check(L.lib().lrt_exchange_bytes(1280, 720, 8, 8, ctypes.byref(d), ctypes.byref(g)))
+    assert d.value == 1280 * 720 * 16
+    assert g.value == 7 * 96 * 1280 * 12
+    L.check(L.lib().lrt_exchange_bytes(1280, 720, 8, 1, ctypes.byref(d), ctypes.byref(g)))
+    assert g.value == 0
+    assert L.lib().lrt_exchange_bytes(1280, 720, 0, 8, ctypes.byref(d), ctypes.byref(g)) != 0

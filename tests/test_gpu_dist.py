@@ -177,3 +177,8 @@ def test_bench_two_ranks_gloo(gpu, scaling, exchange):
         assert d["config"]["spp_total"] == 8
         assert 2.0e7 < d["config"]["rays_per_step"] < 2.6e7   # ~2 x config 2's 11.67 M rays
     assert d["value"] > 0
+    # both exchanges timed in the same line (north_star's RCCL gather beside the IPC stores),
+    # their assembled frames identical bit for bit
+    ex = d["exchange"]
+    assert ex["primary"] == exchange and ex["frames_identical"] is True, ex
+    assert set(ex["legs"]) == {"remote", "rccl"} and all(v["value"] > 0 for v in ex["legs"].values()), ex

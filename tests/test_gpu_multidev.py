@@ -1,13 +1,14 @@
 """GPU tests of round 3's host-side additions, through the C-ABI:
 
 * lrt_initialize_devices: one process splits a host render over several devices
-  (row-block-cyclic) and gathers the shards into the first -- by RCCL (ncclCommInitAll +
+  (row-block-cyclic); each device copies its rows back to the caller's buffer (the direct
+  exchange, default) or the shards' RGB is gathered into the first -- by RCCL (ncclCommInitAll +
   grouped ncclGather, rccl.h:745) when the ids are distinct, by device-to-device copies when an
-  id repeats. On a one-GPU box RCCL runs with one device; the copy exchange rehearses 2-3
-  shards on GPU 0. Every frame must equal the one-device render / the oracle bit for bit
+  id repeats. On a one-GPU box RCCL runs with one device; repeated ids rehearse 2-3 shards on
+  GPU 0. Every frame must equal the one-device render / the oracle bit for bit
   (parallel.cpp:262,280-286 per pixel; the reference's dispatch over rows, :317-320).
-* the registration cache: a pageable DrawTest buffer (main.cpp:40's `new float[]`) is
-  page-locked on its second call and takes the pinned pipeline, same bits.
+* DrawTest keeps nothing of the caller's buffer between calls: a pageable buffer freed and
+  remapped at the same address (main.cpp:40's `new float[]` replaced) renders exactly.
 * the pool kernel's heaviest-first tile order on two streams at once (the bench's
   pipelining), on the exact benchmarked state (order=2), for a new camera (borrowed order),
   and on the full config-3 frame.
@@ -31,11 +32,11 @@ def _bitwise(got, want, what):
 
 
 @contextlib.contextmanager
-def devices(gpu, ids, peer_copy=False):
+def devices(gpu, ids, peer_copy=False, gather=False):
     """Re-initialise the library over `ids` for the block, then back to lrt_initialize."""
     gpu.ShutdownTest()
     try:
-        gpu.InitializeDevices(ids, peer_copy=peer_copy)
+        gpu.InitializeDevices(ids, peer_copy=peer_copy, gather=gather)
         yield
     finally:
         gpu.ShutdownTest()
@@ -50,16 +51,18 @@ def _host(gpu, job, buf=None):
     return buf, rays
 
 
-@pytest.mark.parametrize("ids,peer,exchange", [([0], False, "rccl"), ([0], True, "copy"), ([0, 0], False, "copy"),
-                                               ([0, 0, 0], False, "copy")],
-                         ids=["rccl-1", "copy-1", "copy-2", "copy-3"])
-def test_multidevice_render_host_equals_oracle(gpu, ids, peer, exchange):
+@pytest.mark.parametrize("ids,peer,gather,exchange", [
+    ([0], False, False, "direct"), ([0, 0], False, False, "direct"), ([0, 0, 0], False, False, "direct"),
+    ([0], False, True, "rccl"), ([0], True, False, "copy"), ([0, 0], False, True, "copy"),
+    ([0, 0, 0], False, True, "copy")],
+    ids=["direct-1", "direct-2", "direct-3", "rccl-1", "copy-1", "copy-2", "copy-3"])
+def test_multidevice_render_host_equals_oracle(gpu, ids, peer, gather, exchange):
     from learnraytracing_amd import _lib as L
     w, h, frames, depth = 320, 180, 4, 8
     want, wrays = oracle.orc_render(w, h, frames, depth)
     prev = np.random.default_rng(1).uniform(0, 1, (h, w, 4)).astype(np.float32)
     want_prev, _ = oracle.orc_render(w, h, frames, depth, frame0=3, buf=prev.copy())
-    with devices(gpu, ids, peer):
+    with devices(gpu, ids, peer, gather):
         assert gpu.device_count() == len(ids)
         buf, rays = _host(gpu, gpu.Job(width=w, height=h, frames=frames, max_depth=depth))
         info = L.last_launch()
@@ -74,8 +77,9 @@ def test_multidevice_render_host_equals_oracle(gpu, ids, peer, exchange):
         assert np.array_equal(b2[..., 3].view(np.uint32), prev[..., 3].view(np.uint32))
 
 
-@pytest.mark.parametrize("ids", [[0], [0, 0, 0]], ids=["rccl-1", "copy-3"])
-def test_multidevice_drawtest_window_bvh(gpu, ids):
+@pytest.mark.parametrize("ids,gather", [([0], True), ([0, 0, 0], True), ([0, 0, 0], False)],
+                         ids=["rccl-1", "copy-3", "direct-3"])
+def test_multidevice_drawtest_window_bvh(gpu, ids, gather):
     """DrawTest (kMaxDepth 20) progressively, a window with odd sizes, and a BVH scene
     rendered over the devices: all equal the oracle."""
     from learnraytracing_amd.scene import random_scene, scene_arrays
@@ -87,7 +91,7 @@ def test_multidevice_drawtest_window_bvh(gpu, ids):
     sph, mat = random_scene(300, 4)
     s, m = (np.array(v, np.float32) for v in scene_arrays(sph, mat))
     wbvh, wbr = oracle.orc_render(160, 90, 5, 8, spheres=s, mats=m)
-    with devices(gpu, ids):
+    with devices(gpu, ids, gather=gather):
         bb = np.zeros(w * h * 4, np.float32)
         for f in range(2):
             assert gpu.DrawTest(0.0, f, w, h, bb) > 0
@@ -99,6 +103,24 @@ def test_multidevice_drawtest_window_bvh(gpu, ids):
         img, r = _host(gpu, gpu.Job(width=160, height=90, frames=5, max_depth=8))
         _bitwise(img, wbvh, "multi-device BVH scene")
         assert r == wbr
+
+
+@pytest.mark.parametrize("gather", [False, True], ids=["direct", "gather"])
+def test_multidevice_drawtest_1280x720_three_frames(gpu, gather):
+    """The reference caller's own shape on two devices (GPU 0 twice on a one-GPU box):
+    DrawTest at 1280x720, kMaxDepth 20, frames 0-2 into one pageable buffer, each frame's rows
+    split over the devices -- equal to the oracle bit for bit, rays included."""
+    from learnraytracing_amd import _lib as L
+    w, h = 1280, 720
+    want = np.zeros((h, w, 4), np.float32)
+    wr = [oracle.orc_render(w, h, 1, 20, frame0=f, buf=want, threads=16)[1] for f in range(3)]
+    with devices(gpu, [0, 0], gather=gather):
+        bb = np.zeros(w * h * 4, np.float32)
+        got = [gpu.DrawTest(0.0, f, w, h, bb) for f in range(3)]
+        info = L.last_launch()
+    assert info["devices"] == "2" and info["exchange"] == ("copy" if gather else "direct"), info
+    assert got == wr
+    _bitwise(bb.reshape(h, w, 4), want, "two-device DrawTest 1280x720")
 
 
 def test_multidevice_caller_shard_stays_on_first_device(gpu):
