@@ -85,6 +85,9 @@ int order_alloc(Context::TileOrder& e, long long ntiles, hipStream_t s) {
     e.d_tmp = b + 4 * arr;
     e.tmp_bytes = tmp;
     LRT_HIP(fill_iota(e.d_ids, (int)cap, s));
+    // a later signature may take this entry on another stream, whose sort reads d_ids: the
+    // fill completes here (allocation is rare -- the first use sizes every entry at once)
+    LRT_HIP(hipStreamSynchronize(s));
     e.cap = cap;
     return LRT_OK;
 }

@@ -53,8 +53,13 @@ typedef const KernelArgs* KArgPtr;
 __device__ __forceinline__ KArgPtr opaque_args() { return nullptr; }
 #endif
 
+// Waves per SIMD the grid instances are compiled for (LRT_POOL_GRID_WAVES, A/B)
+#ifndef LRT_POOL_GRID_WAVES
+#define LRT_POOL_GRID_WAVES LRT_V0_WAVES_PER_EU
+#endif
 template <int MAXD, bool kLds, int kAcc, int kPix, int kNS = 0>
-__global__ __launch_bounds__(64, LRT_V0_WAVES_PER_EU) void pool_kernel(const KernelArgs a) {
+__global__ __launch_bounds__(64, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0_WAVES_PER_EU) void pool_kernel(
+    const KernelArgs a) {
     static_assert(kNS == 0 || (kLds && !kAcc), "a fixed sphere count is for the LDS linear scan");
     // LDS as trace_kernel: [recursion stack kTraceLdsLevels x 64][powf tables][renormalize
     // table unless kAcc][spheres][materials][lights][bvh stack at a.bvh_stack_offset]

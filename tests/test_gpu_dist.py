@@ -182,3 +182,41 @@ def test_bench_two_ranks_gloo(gpu, scaling, exchange):
     ex = d["exchange"]
     assert ex["primary"] == exchange and ex["frames_identical"] is True, ex
     assert set(ex["legs"]) == {"remote", "rccl"} and all(v["value"] > 0 for v in ex["legs"].values()), ex
+
+
+@pytest.mark.parametrize("kernel,scene", [("pool", "default"), ("wavefront", "default"), ("pool", "scene1000"),
+                                          ("v0", "scene1000"), ("pool-bvh", "scene1000")])
+def test_fused_frame_store_every_kernel(gpu, kernel, scene):
+    """The fused exchange's frame stores (lrt_render_device_to_frame) in every kernel that has
+    them -- pool_kernel's round lerp, the wavefront merge (merge_samples, pix0 / GlobalRow), v0
+    -- on row-block-cyclic shards of a window with x0, y0 != 0, on the reference scene and on
+    the 1000-sphere scene (grid and BVH): the frame the shards assemble in place equals
+    render_host's window bit for bit (advisor r3: the pool and wavefront stores were never
+    compared with a plain render)."""
+    import torch
+
+    from learnraytracing_amd.scene import random_scene
+    flags = {"pool": 512, "wavefront": 256, "v0": 2, "pool-bvh": 512 | 1024}[kernel]
+    W, H = (640, 360) if scene == "default" else (3840, 2160)
+    x0, xc, y0, yc, rb, period = 37, 256, 21, 133, 8, 3
+    frames, depth = (4, 8) if scene == "default" else (8, 8)
+    if scene == "scene1000":
+        gpu.set_scene(*random_scene(1000, 1))
+    try:
+        want = np.zeros((yc, xc, 4), np.float32)
+        gpu.render_host(gpu.Job(width=W, height=H, frames=frames, max_depth=depth, x0=x0, x_count=xc, y0=y0,
+                                row_count=yc, flags=flags), want)
+        frame = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        rays = torch.zeros(1, dtype=torch.int64, device="cuda")
+        for ph in range(period):
+            rows = sum(1 for ly in range(yc) if (ly // rb) % period == ph)
+            job = gpu.Job(width=W, height=H, frames=frames, max_depth=depth, x0=x0, x_count=xc, y0=y0,
+                          row_count=rows, row_block=rb, row_period=period, row_phase=ph, flags=flags)
+            buf = torch.zeros((rows, xc, 4), dtype=torch.float32, device="cuda")
+            gpu.render_tensor_to_frame(job, buf, rays, frame.data_ptr())
+        torch.cuda.synchronize()
+        got = frame[y0:y0 + yc, x0:x0 + xc].cpu().numpy()
+    finally:
+        if scene == "scene1000":
+            gpu.set_scene(*gpu.default_scene())
+    assert np.array_equal(got[..., :3].view(np.uint32), want[..., :3].view(np.uint32)), kernel
