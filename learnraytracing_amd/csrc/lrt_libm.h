@@ -21,7 +21,7 @@
 //
 // Table values are those of glibc 2.35's __sincosf_table, __powf_log2_data and
 // __exp2f_data (identical to optimized-routines' sincosf_data.c, powf_log2_data.c,
-// exp2f_data.c).
+// exp2f_data.c; Copyright (c) Arm Limited, MIT licence -- see THIRD_PARTY_NOTICES.md).
 #pragma once
 #include <stdint.h>
 
