@@ -107,7 +107,7 @@ struct KernelArgs {
     int regenMin;                 // v5: waiting lanes that trigger a refill
     const float* lerp;            // lerpFac = (float)f / (float)(f + 1) for f < kLerpTable (parallel.cpp:262)
     float4* samp;                 // sample mode: frames planes of xc * rows colours
-    float4* colbuf;               // v5 (pool): poolSlots colour slots per block
+    float* colbuf;                // v5 (pool): poolSlots colour slots (RGB) per block
     int poolSlots;
     const int* perm;              // v5: queue position -> tile, heaviest measured tiles first (null: identity)
     unsigned* tcost;              // v5: per-tile cost recording (100 MHz ticks of the tile's wave), or null

@@ -18,7 +18,7 @@
 // frame-by-frame loop -- and the next round (or tile) starts.
 //
 // Same per-ray arithmetic, RNG streams (PixelSeed(x, y, f)), draw order, ray counting,
-// Scatter and recursion fold as Trace (lrt_trace.h). The colour slots (16 B per sample of
+// Scatter and recursion fold as Trace (lrt_trace.h). The colour slots (12 B per sample of
 // a round) live in global memory: LDS already holds the recursion stack.
 #pragma once
 
@@ -53,6 +53,9 @@ typedef const KernelArgs* KArgPtr;
 __device__ __forceinline__ KArgPtr opaque_args() { return nullptr; }
 #endif
 
+#ifndef LRT_POOL_OVF_ZERO
+#define LRT_POOL_OVF_ZERO 1
+#endif
 // Waves per SIMD the grid instances are compiled for (LRT_POOL_GRID_WAVES, A/B)
 #ifndef LRT_POOL_GRID_WAVES
 #define LRT_POOL_GRID_WAVES LRT_V0_WAVES_PER_EU
@@ -116,16 +119,37 @@ __global__ __launch_bounds__(64, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0
     float4* const lstk = smem + lane;   // this lane's recursion stack (LDS)
     const size_t gtid = (size_t)blockIdx.x * 64 + lane;
     const size_t gthreads = (size_t)gridDim.x * 64;
-    float4* const gstk = a.ovf + gtid;   // levels >= kTraceLdsLevels (MAXD > 8)
+    // Levels >= kTraceLdsLevels (MAXD > 8) in the global overflow stack: a u16 per level (the
+    // material id, bit 15 set when the level's matE + lightE is exactly +0, which then needs no
+    // float4 at all -- the fold adds the literal +0 the stored value was, parallel.cpp:214) and
+    // the float4 only for the others. Deep levels are mostly glass and metal chains, whose
+    // events add nothing (LRT_POOL_OVF_ZERO=0: a float4 per level, round 3).
+    float4* const gstk = a.ovf + gtid;
+    unsigned short* const gid =
+        reinterpret_cast<unsigned short*>(a.ovf + gthreads * (size_t)(a.maxDepth - kTraceLdsLevels)) + gtid;
     auto put = [&](int lvl, float4 v) {
-        if (MAXD <= kTraceLdsLevels || lvl < kTraceLdsLevels) lstk[lvl * 64] = v;
-        else gstk[(size_t)(lvl - kTraceLdsLevels) * gthreads] = v;
+        if (MAXD <= kTraceLdsLevels || lvl < kTraceLdsLevels) {
+            lstk[lvl * 64] = v;
+        } else if (LRT_POOL_OVF_ZERO) {
+            const size_t o = (size_t)(lvl - kTraceLdsLevels) * gthreads;
+            const bool z = (__float_as_uint(v.x) | __float_as_uint(v.y) | __float_as_uint(v.z)) == 0u;
+            gid[o] = (unsigned short)(__float_as_int(v.w) | (z ? 0x8000 : 0));
+            if (!z) gstk[o] = v;
+        } else {
+            gstk[(size_t)(lvl - kTraceLdsLevels) * gthreads] = v;
+        }
     };
     auto get = [&](int lvl) -> float4 {
         if (MAXD <= kTraceLdsLevels || lvl < kTraceLdsLevels) return lstk[lvl * 64];
-        return gstk[(size_t)(lvl - kTraceLdsLevels) * gthreads];
+        const size_t o = (size_t)(lvl - kTraceLdsLevels) * gthreads;
+        if (LRT_POOL_OVF_ZERO) {
+            const unsigned t = gid[o];
+            if (t & 0x8000u) return make_float4(0.0f, 0.0f, 0.0f, __int_as_float((int)(t & 0x7fffu)));
+        }
+        return gstk[o];
     };
-    float4* const slots = a.colbuf + (size_t)blockIdx.x * a.poolSlots;   // this wave's colour slots
+    // this wave's colour slots: RGB, 12 B per sample (the 4th float was never read)
+    float* const slots = a.colbuf + (size_t)blockIdx.x * a.poolSlots * 3;
 
     constexpr int TX = PoolTile<kPix>::X, TY = PoolTile<kPix>::Y;
     constexpr int kRoundFrames = kPoolSamples / kPix;
@@ -181,7 +205,9 @@ __global__ __launch_bounds__(64, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0
                             const float4 b = sc.mats[3 * __float_as_int(s.w) + 2];
                             T = f3(s.x, s.y, s.z) + f3(b.x, b.y, b.z) * T;
                         }
-                        slots[k] = make_float4(T.x, T.y, T.z, 0.0f);
+                        slots[3 * k] = T.x;
+                        slots[3 * k + 1] = T.y;
+                        slots[3 * k + 2] = T.z;
                         state = kPoolIdle;
                     }
                     const unsigned long long needM = waitM;
@@ -319,7 +345,8 @@ __global__ __launch_bounds__(64, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0
                     float4 acc = *mpx;
                     F3 c3 = f3(acc.x, acc.y, acc.z);
                     for (int t = 0; t < nfr; ++t) {
-                        const float4 c = slots[t * kPix + j];
+                        const float* const cp = slots + 3 * (t * kPix + j);
+                        const F3 c = f3(cp[0], cp[1], cp[2]);
                         const int f = fr0 + t;
                         const float lerpFac = f < kLerpTable ? lerp[f] : (float)f / (float)(f + 1);
                         c3 = c3 * lerpFac + f3(c.x, c.y, c.z) * (1.0f - lerpFac);

@@ -49,11 +49,13 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
         a.regenMin = env;
     }
     a.poolSlots = kPix * std::min(a.frames, kPoolSamples / kPix);   // one round's samples
-    e = hipMallocAsync((void**)&a.colbuf, sizeof(float4) * (size_t)a.poolSlots * grid.x, s);
+    e = hipMallocAsync((void**)&a.colbuf, sizeof(float) * 3 * (size_t)a.poolSlots * grid.x, s);
     if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(pool colour slots)");
     if (a.maxDepth > kTraceLdsLevels) {
         const size_t gthreads = (size_t)grid.x * 64;
-        e = hipMallocAsync((void**)&a.ovf, sizeof(float4) * gthreads * (size_t)(a.maxDepth - kTraceLdsLevels), s);
+        // float4 levels, then the u16 level tags (lrt_pool.h)
+        e = hipMallocAsync((void**)&a.ovf, (sizeof(float4) + sizeof(unsigned short)) * gthreads *
+                                               (size_t)(a.maxDepth - kTraceLdsLevels), s);
         if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(trace stack overflow)");
     }
 #ifdef LRT_EXP_SECSTATS
