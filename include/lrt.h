@@ -267,12 +267,13 @@ int lrt_stream_destroy(void* stream);
  * (LRT_HOST_ZEROCOPY=0 turns that off). Free with lrt_host_free. */
 int lrt_host_alloc(size_t bytes, void** out);
 int lrt_host_free(void* p);
-/* A PAGEABLE host backbuffer (the reference's `new float[]`, main.cpp:40) that lrt_draw_test
- * sees on two consecutive calls is page-locked in place (hipHostRegister) and from then on
- * takes the page-locked paths; up to 8 such buffers stay registered. The caller must call
- * lrt_host_unregister(buf) before freeing such a buffer while the library is initialised
- * (lrt_shutdown unregisters every one); the reference's caller keeps its buffer for the whole
- * run. lrt_render_host never registers. LRT_HOST_REGISTER=0 keeps pageable buffers staged. */
+/* A PAGEABLE host backbuffer (the reference's `new float[]`, main.cpp:40) is page-locked by
+ * lrt_draw_test / lrt_render_host for the duration of that one call (hipHostRegister when it
+ * starts, hipHostUnregister before it returns) and takes the page-locked paths. The library
+ * keeps nothing of the caller's buffer between calls: the caller may free it, or reuse or
+ * remap its address, at any time between calls -- DrawTest's own contract (parallel.h:8).
+ * LRT_HOST_REGISTER=0 stages pageable buffers instead. lrt_host_unregister is a no-op kept
+ * for callers of the round-3 API (returns LRT_OK). */
 int lrt_host_unregister(void* p);
 
 /* Number of local rows GPU `phase` owns in a row-block-cyclic split of `height` rows
