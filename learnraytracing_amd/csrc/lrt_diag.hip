@@ -169,7 +169,7 @@ int lrt_grid_stats(const lrt_sphere* spheres, int count, const float* rays, int 
     GridHost G;
     build_grid_host(spheres, count, sph, G);
     GridView g;
-    g.cells = G.cells.data();
+    g.cells = G.ranges.data();
     g.rsph = G.rsph.data();
     g.rid = G.rid.data();
     g.bsph = G.bsph.data();

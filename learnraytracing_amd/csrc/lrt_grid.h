@@ -28,7 +28,7 @@
 namespace lrt {
 
 struct GridView {
-    const unsigned* cells;   // ncells + 1 offsets into rsph / rid
+    const uint2* cells;      // per cell: [start, end) of its spheres in rsph / rid
     const float4* rsph;      // cell-ordered sphere copies: float4(center, r^2)
     const int* rid;          // their original indices
     const float4* bsph;      // spheres every ray tests first
@@ -88,7 +88,10 @@ LRT_DEV void GridTest(GridQuery& q, const float4& s, int id) {
 // Starts q's walk along q.d (q.bestT / q.best / q.li set by the caller): the big spheres,
 // then the cell where the ray enters the box.
 LRT_DEV void GridStart(GridQuery& q, const GridView& g, GridStats* st = nullptr) {
-    for (int k = 0; k < g.nbig; ++k) GridTest(q, g.bsph[k], g.bid[k]);
+    // (a shadow query skips its own light: the light's candidate IS the bar, and a tie with the
+    // same index changes nothing -- GridBeats is false for it)
+    for (int k = 0; k < g.nbig; ++k)
+        if (q.best != -2 || g.bid[k] != q.li) GridTest(q, g.bsph[k], g.bid[k]);
     q.inv = f3(rcp_rn(q.d.x), rcp_rn(q.d.y), rcp_rn(q.d.z));
     q.mode = 2;
     if (g.count == 0 || g.nx == 0) return;
@@ -137,9 +140,9 @@ LRT_DEV void GridStart(GridQuery& q, const GridView& g, GridStats* st = nullptr)
             : q.d.y < 0.0f ? (GridPlane(g.loy, q.cy, g.hy) - q.o.y) * q.inv.y : __builtin_inff();
     q.tnz = q.d.z > 0.0f ? (GridPlane(g.loz, q.cz + 1, g.hz) - q.o.z) * q.inv.z
             : q.d.z < 0.0f ? (GridPlane(g.loz, q.cz, g.hz) - q.o.z) * q.inv.z : __builtin_inff();
-    const int c = (q.cz * g.ny + q.cy) * g.nx + q.cx;
-    q.j = g.cells[c];
-    q.jend = g.cells[c + 1];
+    const uint2 cr = g.cells[(q.cz * g.ny + q.cy) * g.nx + q.cx];
+    q.j = cr.x;
+    q.jend = cr.y;
     q.mode = 0;
     if (st) st->cells += 1;
 }
@@ -167,9 +170,9 @@ LRT_DEV void GridAdvance(GridQuery& q, const GridView& g, GridStats* st) {
         if ((unsigned)q.cz >= (unsigned)g.nz) { q.mode = 2; return; }
         q.tnz = (GridPlane(g.loz, q.cz + (q.d.z > 0.0f ? 1 : 0), g.hz) - q.o.z) * q.inv.z;
     }
-    const int c = (q.cz * g.ny + q.cy) * g.nx + q.cx;
-    q.j = g.cells[c];
-    q.jend = g.cells[c + 1];
+    const uint2 cr = g.cells[(q.cz * g.ny + q.cy) * g.nx + q.cx];   // one 8-byte load per cell
+    q.j = cr.x;
+    q.jend = cr.y;
     if (st) st->cells += 1;
 }
 LRT_DEV void GridIter(GridQuery& q, const GridView& g, GridStats* st) {

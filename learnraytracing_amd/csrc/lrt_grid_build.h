@@ -15,7 +15,8 @@
 namespace lrt {
 
 struct GridHost {
-    std::vector<unsigned> cells;   // ncells + 1
+    std::vector<unsigned> cells;   // ncells + 1 (CSR offsets)
+    std::vector<uint2> ranges;     // per cell [cells[c], cells[c + 1]): the device's view
     std::vector<float4> rsph, bsph;
     std::vector<int> rid, bid;
     int nx = 0, ny = 0, nz = 0;
@@ -125,6 +126,7 @@ inline void build_grid_host(const lrt_sphere* s, int n, const std::vector<float4
         }
     if (in.empty()) {   // every sphere is tested first: no walk at all
         G.cells.assign(1, 0u);
+        G.ranges.assign(1, make_uint2(0u, 0u));
         return;
     }
     box_of(in, lo, hi);
@@ -196,6 +198,8 @@ inline void build_grid_host(const lrt_sphere* s, int n, const std::vector<float4
             G.rid.resize(cnt[ncells]);
         }
     }
+    G.ranges.resize(ncells);
+    for (long long c = 0; c < ncells; ++c) G.ranges[c] = make_uint2(G.cells[c], G.cells[c + 1]);
     long long nonempty = 0;
     for (long long c = 0; c < ncells; ++c) {
         const int r = (int)(G.cells[c + 1] - G.cells[c]);

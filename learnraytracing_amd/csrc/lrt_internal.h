@@ -207,7 +207,7 @@ struct Context {
     int bvh_stack_levels = kBvhStackLevels;   // this scene's traversal depth (<= kBvhStackLevels)
     // uniform grid (the same scenes; lrt_grid.h): gv holds the device pointers and geometry,
     // gv.on = built; grid_pick = the policy's choice over the BVH (grid_suitable)
-    unsigned* d_grid_cells = nullptr;
+    uint2* d_grid_cells = nullptr;
     float4* d_grid_rsph = nullptr;
     int* d_grid_rid = nullptr;
     float4* d_grid_bsph = nullptr;

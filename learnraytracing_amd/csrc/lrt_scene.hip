@@ -355,7 +355,7 @@ int upload_scene(Context& c, const lrt_sphere* s, const lrt_material* m, int n) 
         c.bvh_margin = B.margin;
         c.bvh_stack_levels = B.stack_levels;
         c.bvh_on = 1;
-        LRT_HIP(upload(c.d_grid_cells, G.cells));
+        LRT_HIP(upload(c.d_grid_cells, G.ranges));
         LRT_HIP(upload(c.d_grid_rsph, G.rsph));
         LRT_HIP(upload(c.d_grid_rid, G.rid));
         LRT_HIP(upload(c.d_grid_bsph, G.bsph));
