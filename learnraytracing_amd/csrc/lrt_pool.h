@@ -100,7 +100,8 @@ __global__ __launch_bounds__(64, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0
     sc.count = a.count;
     sc.nlights = a.nlights;
     sc.bv = a.bv;
-    sc.gv = a.gv;
+    // (the grid's view is read from the kernel arguments where a walk starts, below: held in
+    // SGPRs for the whole kernel its ~28 scalars spilled the loop's own state)
     sc.bstk = reinterpret_cast<unsigned short*>(reinterpret_cast<char*>(smem) + a.bvh_stack_offset) + lane;
     sc.bstride = 64;
 #ifdef LRT_EXP_SECSTATS
@@ -263,7 +264,8 @@ __global__ __launch_bounds__(64, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0
                     const bool hasS = pend && dl.on;
                     if constexpr (kAcc == kAccGrid) {
                         const float4 ls = hasS ? sc.sph[dl.li] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                        nid = ClosestHitDualGrid(r.orig, r.dir, hasS, dl.l, dl.li, ls, sc.gv, nt, lit);
+                        const GridView gv = opaque_args()->gv;
+                        nid = ClosestHitDualGrid(r.orig, r.dir, hasS, dl.l, dl.li, ls, gv, nt, lit);
                     } else if constexpr (kAcc == kAccBvh) {
                         if (coherent) {
                             nid = ClosestHitBVH(r.orig, r.dir, sc.bv, nt, sc.bstk, sc.bstride, nullptr, true);
@@ -301,6 +303,7 @@ __global__ __launch_bounds__(64, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0
                         if (depth < a.maxDepth) {
                             F3 lightE;
                             dl.on = false;
+                            if constexpr (kAcc == kAccGrid) sc.gv = opaque_args()->gv;   // other lights' shadow rays
                             const F3 X = ScatterDir<kAcc, kNS>(mat, nid, r, rec, lightE, rays, rng, sc, &dl, coherent);
                             sec_count(sc, kSecPost);
                             const F3 dir = renormalize(normalize(X), sc.rnlut);   // Ray(rec.pos, normalize(X))
