@@ -20,7 +20,7 @@
 // sphere instead (origins more than ~8 scene sizes away). No stack: the walk's state is a
 // cell and three plane times, so the traversal holds fewer registers than the BVH's and no LDS.
 //
-// Walk and sphere tests share ONE loop (GridStep): an iteration advances to the next cell
+// Walk and sphere tests share ONE loop (GridIter): an iteration advances to the next cell
 // when the current cell's list is used up, then tests one sphere. A wave therefore runs max
 // over lanes of (cells + spheres) iterations, not the sum of per-cell maxima.
 #pragma once
@@ -103,8 +103,6 @@ LRT_DEV void GridStart(GridQuery& q, const GridView& g, GridStats* st = nullptr)
     if (!((mo + g.ext) * 1.52587890625e-05f < g.errk)) {
         if (st) st->fallback += 1;
         q.mode = 1;
-        q.j = 0;
-        q.jend = (unsigned)g.count;
         return;
     }
     const float hix = GridPlane(g.lox, g.nx, g.hx), hiy = GridPlane(g.loy, g.ny, g.hy),
@@ -140,7 +138,7 @@ LRT_DEV void GridStart(GridQuery& q, const GridView& g, GridStats* st = nullptr)
             : q.d.y < 0.0f ? (GridPlane(g.loy, q.cy, g.hy) - q.o.y) * q.inv.y : __builtin_inff();
     q.tnz = q.d.z > 0.0f ? (GridPlane(g.loz, q.cz + 1, g.hz) - q.o.z) * q.inv.z
             : q.d.z < 0.0f ? (GridPlane(g.loz, q.cz, g.hz) - q.o.z) * q.inv.z : __builtin_inff();
-    const uint2 cr = g.cells[(q.cz * g.ny + q.cy) * g.nx + q.cx];
+    const uint2 cr = g.cells[(unsigned)((q.cz * g.ny + q.cy) * g.nx + q.cx)];
     q.j = cr.x;
     q.jend = cr.y;
     q.mode = 0;
@@ -148,55 +146,66 @@ LRT_DEV void GridStart(GridQuery& q, const GridView& g, GridStats* st = nullptr)
 }
 
 // One iteration of q's query: the next cell if the current one is used up (or the end of the
-// walk), then one sphere test.
+// walk), then one sphere test. The step is straight-line code: the axis with the nearest
+// plane (x, then y, then z on ties) is selected rather than branched on, so a wave whose
+// lanes step along different axes issues one sequence, not three.
 LRT_DEV void GridAdvance(GridQuery& q, const GridView& g, GridStats* st) {
     if (q.mode != 0 || q.j < q.jend) return;
     const float T = __builtin_fminf(__builtin_fminf(q.tnx, q.tny), q.tnz);
-    if (q.bestT < T - (g.pad + 1e-5f * T)) {   // nothing beyond this cell can win or tie
+    // nothing beyond this cell can win or tie (or T is NaN: nowhere to go)
+    if (q.bestT < T - (g.pad + 1e-5f * T) || !(T == T)) {
         q.mode = 2;
         return;
     }
-    if (q.tnx == T) {
-        q.cx += q.d.x > 0.0f ? 1 : -1;
-        if ((unsigned)q.cx >= (unsigned)g.nx) { q.mode = 2; return; }
-        q.tnx = (GridPlane(g.lox, q.cx + (q.d.x > 0.0f ? 1 : 0), g.hx) - q.o.x) * q.inv.x;
-    } else if (q.tny == T) {
-        q.cy += q.d.y > 0.0f ? 1 : -1;
-        if ((unsigned)q.cy >= (unsigned)g.ny) { q.mode = 2; return; }
-        q.tny = (GridPlane(g.loy, q.cy + (q.d.y > 0.0f ? 1 : 0), g.hy) - q.o.y) * q.inv.y;
-    } else {
-        if (!(q.tnz == T)) { q.mode = 2; return; }   // all three infinite / NaN: nowhere to go
-        q.cz += q.d.z > 0.0f ? 1 : -1;
-        if ((unsigned)q.cz >= (unsigned)g.nz) { q.mode = 2; return; }
-        q.tnz = (GridPlane(g.loz, q.cz + (q.d.z > 0.0f ? 1 : 0), g.hz) - q.o.z) * q.inv.z;
+    const bool ax = q.tnx == T, ay = !ax && q.tny == T, az = !ax && !ay;
+    const float inv = ax ? q.inv.x : ay ? q.inv.y : q.inv.z;
+    const int up = inv > 0.0f ? 1 : 0;   // the ray moves up this axis (inv has d's sign)
+    const int c = (ax ? q.cx : ay ? q.cy : q.cz) + (up ? 1 : -1);
+    const int n = ax ? g.nx : ay ? g.ny : g.nz;
+    if ((unsigned)c >= (unsigned)n) {   // left the box
+        q.mode = 2;
+        return;
     }
-    const uint2 cr = g.cells[(q.cz * g.ny + q.cy) * g.nx + q.cx];   // one 8-byte load per cell
+    q.cx = ax ? c : q.cx;
+    q.cy = ay ? c : q.cy;
+    q.cz = az ? c : q.cz;
+    const float lo = ax ? g.lox : ay ? g.loy : g.loz;
+    const float h = ax ? g.hx : ay ? g.hy : g.hz;
+    const float o = ax ? q.o.x : ay ? q.o.y : q.o.z;
+    const float tn = (GridPlane(lo, c + up, h) - o) * inv;   // the same expression GridStart uses
+    q.tnx = ax ? tn : q.tnx;
+    q.tny = ay ? tn : q.tny;
+    q.tnz = az ? tn : q.tnz;
+    const uint2 cr = g.cells[(unsigned)((q.cz * g.ny + q.cy) * g.nx + q.cx)];   // one 8-byte load per cell
     q.j = cr.x;
     q.jend = cr.y;
     if (st) st->cells += 1;
 }
+// The fallback (mode 1): the whole scene in index order, the reference's own scan.
+LRT_DEV void GridScanAll(GridQuery& q, const GridView& g, GridStats* st) {
+    for (int i = 0; i < g.count; ++i) GridTest(q, g.all[i], i);
+    if (st) st->spheres += g.count;
+    q.mode = 2;
+}
 LRT_DEV void GridIter(GridQuery& q, const GridView& g, GridStats* st) {
+    if (__builtin_expect(q.mode == 1, 0)) {   // never in practice (origins ~8 scene sizes away)
+        GridScanAll(q, g, st);
+        return;
+    }
     GridAdvance(q, g, st);
-    if (q.mode != 2 && q.j < q.jend) {
+    if (q.mode == 0 && q.j < q.jend) {
         if (st) st->spheres += 1;
         const unsigned j = q.j++;
-        if (q.mode == 0) {
-            const float4 s = g.rsph[j];
-            const float cand = GridCand(q.o, q.d, s);
-            // the original index is read only when it can matter (a win or an exact tie)
-            if (cand < q.bestT || (cand == q.bestT && q.best != -1)) {
-                const int id = g.rid[j];
-                if (GridBeats(q, cand, id)) {
-                    q.bestT = cand;
-                    q.best = id;
-                }
+        const float4 s = g.rsph[j];
+        const float cand = GridCand(q.o, q.d, s);
+        // the original index is read only when it can matter (a win or an exact tie)
+        if (cand < q.bestT || (cand == q.bestT && q.best != -1)) {
+            const int id = g.rid[j];
+            if (GridBeats(q, cand, id)) {
+                q.bestT = cand;
+                q.best = id;
             }
-        } else {
-            GridTest(q, g.all[j], (int)j);
-            if (q.j >= q.jend) q.mode = 2;
         }
-    } else if (q.mode == 1) {
-        q.mode = 2;
     }
 }
 
