@@ -103,6 +103,8 @@ LRT_DEV void GridStart(GridQuery& q, const GridView& g, GridStats* st = nullptr)
     if (!((mo + g.ext) * 1.52587890625e-05f < g.errk)) {
         if (st) st->fallback += 1;
         q.mode = 1;
+        q.j = 0;
+        q.jend = (unsigned)g.count;
         return;
     }
     const float hix = GridPlane(g.lox, g.nx, g.hx), hiy = GridPlane(g.loy, g.ny, g.hy),
@@ -158,54 +160,48 @@ LRT_DEV void GridAdvance(GridQuery& q, const GridView& g, GridStats* st) {
         return;
     }
     const bool ax = q.tnx == T, ay = !ax && q.tny == T, az = !ax && !ay;
-    const float inv = ax ? q.inv.x : ay ? q.inv.y : q.inv.z;
-    const int up = inv > 0.0f ? 1 : 0;   // the ray moves up this axis (inv has d's sign)
-    const int c = (ax ? q.cx : ay ? q.cy : q.cz) + (up ? 1 : -1);
-    const int n = ax ? g.nx : ay ? g.ny : g.nz;
-    if ((unsigned)c >= (unsigned)n) {   // left the box
-        q.mode = 2;
+    // each axis updates itself under its own condition (a select between an axis's new and old
+    // value; selecting between fields instead turned into pointer selects, and the query into
+    // scratch memory)
+    const int ux = q.inv.x > 0.0f ? 1 : 0, uy = q.inv.y > 0.0f ? 1 : 0, uz = q.inv.z > 0.0f ? 1 : 0;
+    q.cx += ax ? 2 * ux - 1 : 0;
+    q.cy += ay ? 2 * uy - 1 : 0;
+    q.cz += az ? 2 * uz - 1 : 0;
+    if ((unsigned)q.cx >= (unsigned)g.nx || (unsigned)q.cy >= (unsigned)g.ny || (unsigned)q.cz >= (unsigned)g.nz) {
+        q.mode = 2;   // left the box
         return;
     }
-    q.cx = ax ? c : q.cx;
-    q.cy = ay ? c : q.cy;
-    q.cz = az ? c : q.cz;
-    const float lo = ax ? g.lox : ay ? g.loy : g.loz;
-    const float h = ax ? g.hx : ay ? g.hy : g.hz;
-    const float o = ax ? q.o.x : ay ? q.o.y : q.o.z;
-    const float tn = (GridPlane(lo, c + up, h) - o) * inv;   // the same expression GridStart uses
-    q.tnx = ax ? tn : q.tnx;
-    q.tny = ay ? tn : q.tny;
-    q.tnz = az ? tn : q.tnz;
+    // the stepped axis' next plane, the same expression GridStart uses
+    q.tnx = ax ? (GridPlane(g.lox, q.cx + ux, g.hx) - q.o.x) * q.inv.x : q.tnx;
+    q.tny = ay ? (GridPlane(g.loy, q.cy + uy, g.hy) - q.o.y) * q.inv.y : q.tny;
+    q.tnz = az ? (GridPlane(g.loz, q.cz + uz, g.hz) - q.o.z) * q.inv.z : q.tnz;
     const uint2 cr = g.cells[(unsigned)((q.cz * g.ny + q.cy) * g.nx + q.cx)];   // one 8-byte load per cell
     q.j = cr.x;
     q.jend = cr.y;
     if (st) st->cells += 1;
 }
-// The fallback (mode 1): the whole scene in index order, the reference's own scan.
-LRT_DEV void GridScanAll(GridQuery& q, const GridView& g, GridStats* st) {
-    for (int i = 0; i < g.count; ++i) GridTest(q, g.all[i], i);
-    if (st) st->spheres += g.count;
-    q.mode = 2;
-}
+// The fallback (mode 1, never in practice: origins ~8 scene sizes away) runs through the same
+// sphere test over the whole scene in index order (the reference's own scan, index = position):
+// one copy of the test in the loop.
 LRT_DEV void GridIter(GridQuery& q, const GridView& g, GridStats* st) {
-    if (__builtin_expect(q.mode == 1, 0)) {   // never in practice (origins ~8 scene sizes away)
-        GridScanAll(q, g, st);
-        return;
-    }
     GridAdvance(q, g, st);
-    if (q.mode == 0 && q.j < q.jend) {
+    if (q.mode != 2 && q.j < q.jend) {
         if (st) st->spheres += 1;
         const unsigned j = q.j++;
-        const float4 s = g.rsph[j];
+        const bool scan = q.mode == 1;
+        const float4 s = (scan ? g.all : g.rsph)[j];
         const float cand = GridCand(q.o, q.d, s);
         // the original index is read only when it can matter (a win or an exact tie)
         if (cand < q.bestT || (cand == q.bestT && q.best != -1)) {
-            const int id = g.rid[j];
+            const int id = scan ? (int)j : g.rid[j];
             if (GridBeats(q, cand, id)) {
                 q.bestT = cand;
                 q.best = id;
             }
         }
+        if (scan && q.j >= q.jend) q.mode = 2;
+    } else if (q.mode == 1) {
+        q.mode = 2;
     }
 }
 

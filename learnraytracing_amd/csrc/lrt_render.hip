@@ -339,6 +339,7 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     a.poolSlots = 0;
     a.perm = nullptr;
     a.tcost = nullptr;
+    a.pxcost = nullptr;
     a.samp = colours_out;
     a.sampOnly = colours_out ? 1 : 0;
     a.frame = reinterpret_cast<float4*>(frame);
