@@ -71,7 +71,6 @@ void free_context(Context& c) {
     if (c.d_col) (void)hipFree(c.d_col);
     for (auto& o : c.order) {
         if (o.d_base) (void)hipFree(o.d_base);
-        if (o.d_px) (void)hipFree(o.d_px);
         if (o.ev_rec) (void)hipEventDestroy(o.ev_rec);
         for (auto& u : o.uses) (void)hipEventDestroy(u.second);
     }

@@ -111,9 +111,6 @@ struct KernelArgs {
     int poolSlots;
     const int* perm;              // v5: queue position -> tile, heaviest measured tiles first (null: identity)
     unsigned* tcost;              // v5: per-tile cost recording (100 MHz ticks of the tile's wave), or null
-    unsigned char* pxcost;        // v5: per-pixel cost of the window (scatter events of its samples in the
-                                  // last launch of the signature, saturated at 255) -- read to order a
-                                  // tile's samples heaviest pixel first, rewritten; null: frame-major order
     int sampOnly;                 // colours only (the pipelined host path): samp is the caller's
     float4* frame;                // lrt_render_device_to_frame: the whole width x height frame (any
                                   // device, IPC/peer-mapped) that each finished pixel is also stored
@@ -181,8 +178,6 @@ struct Context {
         unsigned* d_keys = nullptr;
         int* d_ids = nullptr;          // 0..cap-1
         int* d_perm = nullptr;         // written once (by the sort), read by every later launch
-        unsigned char* d_px = nullptr; // per-pixel costs (KernelArgs::pxcost) of the signature's window
-        size_t px_cap = 0;
         void* d_tmp = nullptr;
         size_t tmp_bytes = 0;
         hipEvent_t ev_rec = nullptr;   // after the recording launch and the sort behind it
@@ -370,7 +365,6 @@ int launch_pool_d64(const KernelArgs& a, bool lds, int xc, int rows, int frames,
 
 // ---- lrt_order.hip
 bool pool_order_on();
-bool pool_pxorder_on();
 int pool_probe_mode();
 int order_used(Context::TileOrder& e, hipStream_t s);
 int tile_order(KernelArgs& a, int kPix, long long ntiles, bool& record, Context::TileOrder* users[2], hipStream_t s);

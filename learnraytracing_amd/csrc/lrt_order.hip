@@ -23,15 +23,6 @@ uint64_t fnv(uint64_t h, const void* p, size_t n) {
     for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
     return h;
 }
-// LRT_POOL_PXORDER=0: the pool kernel hands out a tile's samples frame-major (round 3)
-// instead of heaviest pixel first (lrt_pool.h)
-bool pool_pxorder_on() {
-    static const bool on = [] {
-        const char* e = getenv("LRT_POOL_PXORDER");
-        return !(e && atoi(e) == 0);
-    }();
-    return on;
-}
 bool pool_order_on() {
     static const bool on = [] {
         const char* e = getenv("LRT_POOL_ORDER");
@@ -143,18 +134,6 @@ int tile_order(KernelArgs& a, int kPix, long long ntiles, bool& record, Context:
                     if (int rc = order_alloc(o, ntiles, s)) return rc;
         }
         if (!e->ev_rec) LRT_HIP(hipEventCreateWithFlags(&e->ev_rec, hipEventDisableTiming));
-        // the per-pixel costs (the pool kernel's sample order within a tile): a new window that
-        // outgrows the entry's buffer gets a zeroed one (zero costs: frame-major order); the
-        // previous signature's launches have passed (order_release above)
-        const size_t npix = (size_t)a.xc * (size_t)a.rows;
-        if (pool_pxorder_on() && e->px_cap < npix) {
-            if (e->d_px) (void)hipFree(e->d_px);
-            e->d_px = nullptr;
-            e->px_cap = 0;
-            if (hipMalloc((void**)&e->d_px, npix) != hipSuccess) return fail(LRT_E_NOMEM, "hipMalloc(pixel costs)");
-            LRT_HIP(hipMemsetAsync(e->d_px, 0, npix, s));
-            e->px_cap = npix;
-        }
         e->sig = sig;
         e->gkey = gkey;
         e->ntiles = ntiles;
@@ -176,7 +155,6 @@ int tile_order(KernelArgs& a, int kPix, long long ntiles, bool& record, Context:
     }
     users[0] = e;
     e->tick = ++c.order_tick;
-    a.pxcost = (pool_pxorder_on() && e->px_cap >= (size_t)a.xc * (size_t)a.rows) ? e->d_px : nullptr;
     return LRT_OK;
 }
 

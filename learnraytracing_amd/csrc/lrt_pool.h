@@ -118,8 +118,6 @@ __global__ __launch_bounds__(64, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0
     const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
 #endif
     float4* const lstk = smem + lane;   // this lane's recursion stack (LDS)
-    __shared__ unsigned char s_pxperm[64];   // the round's pixels by rank (heaviest first)
-    __shared__ unsigned s_pxcost[64];        // the round's scatter events per pixel
     const size_t gtid = (size_t)blockIdx.x * 64 + lane;
     const size_t gthreads = (size_t)gridDim.x * 64;
     // Levels >= kTraceLdsLevels (MAXD > 8) in the global overflow stack: a u16 per level (the
@@ -178,35 +176,6 @@ __global__ __launch_bounds__(64, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0
         for (int fr0 = a.frame0; fr0 < fend; fr0 += kRoundFrames) {
             const int nfr = fend - fr0 < kRoundFrames ? fend - fr0 : kRoundFrames;
             const int N = nfr * kPix;   // this round's pool
-            // The order the round's samples are handed out in. A round ends with most lanes idle
-            // while its last paths finish (the drain: config 2 at 4 spp runs ~20 % below the same
-            // kernel at 64 spp), and a glass pixel's paths are several times a diffuse one's. With
-            // the pixels' costs from the last launch of this render (a.pxcost: the scatter events
-            // of their samples), all samples of the heaviest pixel go first and the cheapest last,
-            // so the paths still running when the pool runs dry are short ones. Ranks come from
-            // log2 cost classes (ballots), ties in pixel order; without costs: frame-major. Only
-            // which lane traces which sample, and when, changes: every sample keeps its seed and
-            // slot, and the lerp runs in frame order, so the bits are the same.
-            const bool pxo = kPix <= 64 && a.pxcost != nullptr;
-            if (kPix <= 64 && pxo) {
-                const int jj = lane;
-                const int lx = tx0 + jj % TX, ly = ty0 + jj / TX;
-                const KArgPtr pa = opaque_args();
-                const bool in = jj < kPix && lx < pa->xc && ly < pa->rows;
-                const unsigned c = in ? (unsigned)pa->pxcost[(size_t)ly * pa->xc + lx] : 0u;
-                const int cls = in ? (c ? 32 - __builtin_clz(c) : 0) : -1;   // 0..8, -1: no pixel
-                int rank = 0, base = 0;
-                for (int cl = 8; cl >= -1; --cl) {
-                    const unsigned long long m = __ballot(cls == cl);
-                    if (cls == cl) rank = base + __popcll(m & below);
-                    base += __popcll(m);
-                }
-                s_pxperm[rank] = (unsigned char)jj;
-                s_pxcost[jj] = 0u;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            }
             int next = 0, state = kPoolIdle, k = 0, depth = 0;
             bool prevLambert = false;
             uint32_t rng = 1;
@@ -240,26 +209,14 @@ __global__ __launch_bounds__(64, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0
                         slots[3 * k] = T.x;
                         slots[3 * k + 1] = T.y;
                         slots[3 * k + 2] = T.z;
-                        if (kPix <= 64 && pxo) atomicAdd(&s_pxcost[k % kPix], (unsigned)depth + 1u);
                         state = kPoolIdle;
                     }
                     const unsigned long long needM = waitM;
                     if (state == kPoolIdle) {
-                        const int kk = next + __popcll(needM & below);   // issue position in the pool
+                        k = next + __popcll(needM & below);
                         state = kPoolDone;
-                        if (kk < N) {
-                            // the sample at issue position kk: heaviest pixel first (all its
-                            // frames), or frame-major; k = its slot (frame-major, for the lerp)
-                            int j, t;
-                            if (kPix <= 64 && pxo) {
-                                j = s_pxperm[kk / nfr];
-                                t = kk % nfr;
-                            } else {
-                                j = kk % kPix;
-                                t = kk / kPix;
-                            }
-                            k = t * kPix + j;
-                            const int f = fr0 + t;
+                        if (k < N) {
+                            const int j = k % kPix, f = fr0 + k / kPix;
                             const int lx = tx0 + j % TX, ly = ty0 + j / TX;
                             const KArgPtr pa = opaque_args();   // window and camera, read here
                             if (lx < pa->xc && ly < pa->rows) {   // TraceRowJob's per-pixel body (:270-279)
@@ -401,10 +358,6 @@ __global__ __launch_bounds__(64, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0
                     acc.y = c3.y;
                     acc.z = c3.z;
                     *mpx = acc;   // alpha as read
-                    if (kPix <= 64 && pxo) {   // this round's costs, for the next launch's order
-                        const unsigned cst = s_pxcost[j];
-                        pa->pxcost[(size_t)my * xc + mx] = (unsigned char)(cst < 255u ? cst : 255u);
-                    }
                     if (frame) {   // the exchange, fused: the pixel at its global row (GlobalRow)
                         const int rb = pa->rb;
                         const int gy = pa->y0 + (my / rb) * rb * pa->rp + pa->rph * rb + my % rb;

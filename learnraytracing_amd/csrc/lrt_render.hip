@@ -269,6 +269,8 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     if (rc) return rc;
     if (!ctx().ready) return fail(LRT_E_STATE, "lrt_initialize() has not been called");
     if (!d_buf || !d_rays) return fail(LRT_E_INVALID, "device buffer / ray counter is NULL");
+    if (d->flags & (LRT_F_V1 | LRT_F_V2S | LRT_F_V2 | LRT_F_V3))   // (every path, the colours-only one too)
+        return fail(LRT_E_INVALID, "LRT_F_V1/LRT_F_V2S/LRT_F_V2/LRT_F_V3 kernels were removed (the default picks v0 or v5)");
     if (d->x_count == 0 || d->row_count == 0 || d->frames == 0) return LRT_OK;
     KernelArgs a;
     const lrt_camera& c = d->camera;
@@ -339,7 +341,6 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     a.poolSlots = 0;
     a.perm = nullptr;
     a.tcost = nullptr;
-    a.pxcost = nullptr;
     a.samp = colours_out;
     a.sampOnly = colours_out ? 1 : 0;
     a.frame = reinterpret_cast<float4*>(frame);
@@ -350,8 +351,6 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
         if (d->max_depth <= 8) return launch_v0_d8(a, lds, d->x_count, d->row_count, d->frames, false, true, s);
         return launch_v0_d64(a, lds, d->x_count, d->row_count, d->frames, false, true, s);
     }
-    if (d->flags & (LRT_F_V1 | LRT_F_V2S | LRT_F_V2 | LRT_F_V3))
-        return fail(LRT_E_INVALID, "LRT_F_V1/LRT_F_V2S/LRT_F_V2/LRT_F_V3 kernels were removed (the default picks v0 or v5)");
     int kflags = d->flags & (LRT_F_SIMPLE | LRT_F_WAVEFRONT | LRT_F_POOL);
     if (kflags == 0) kflags = auto_kernel(a, d, want_feat);
     if (want_feat && !(kflags & LRT_F_SIMPLE))
