@@ -168,31 +168,7 @@ int lrt_grid_stats(const lrt_sphere* spheres, int count, const float* rays, int 
     }
     GridHost G;
     build_grid_host(spheres, count, sph, G);
-    GridView g;
-    g.cells = G.ranges.data();
-    g.rsph = G.rsph.data();
-    g.rid = G.rid.data();
-    g.bsph = G.bsph.data();
-    g.bid = G.bid.data();
-    g.all = sph.data();
-    g.nbig = (int)G.bsph.size();
-    g.count = G.nx > 0 ? count : 0;
-    g.nx = G.nx;
-    g.ny = G.ny;
-    g.nz = G.nz;
-    g.lox = G.lo[0];
-    g.loy = G.lo[1];
-    g.loz = G.lo[2];
-    g.hx = G.h[0];
-    g.hy = G.h[1];
-    g.hz = G.h[2];
-    g.ihx = G.ih[0];
-    g.ihy = G.ih[1];
-    g.ihz = G.ih[2];
-    g.pad = G.pad;
-    g.errk = G.errk;
-    g.ext = G.ext;
-    g.on = 1;
+    const GridView g = grid_view_host(G, sph.data());
     double sc = 0, ss = 0, mx = 0, bad = 0, fb = 0;
     for (int i = 0; i < n; ++i) {
         const Ray r = make_ray(f3(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]),

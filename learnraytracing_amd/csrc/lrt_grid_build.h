@@ -4,6 +4,7 @@
 #pragma once
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <string>
 #include <vector>
@@ -11,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include "lrt.h"
+#include "lrt_trace.h"
 
 namespace lrt {
 
@@ -28,16 +30,9 @@ struct GridHost {
     int max_refs = 0;
 };
 
-// Cells per sphere (LRT_GRID_DENSITY, default 2): more cells, fewer spheres per cell but more
-// cell steps per ray.
-inline float grid_density() {
-    const char* e = getenv("LRT_GRID_DENSITY");
-    const float v = e ? (float)atof(e) : 2.0f;
-    return v > 0.05f && v < 64.0f ? v : 2.0f;
-}
-
-// s: the scene (center, radius); sph: its device form float4(center, r^2).
-inline void build_grid_host(const lrt_sphere* s, int n, const std::vector<float4>& sph, GridHost& G) {
+// s: the scene (center, radius); sph: its device form float4(center, r^2); density: cells per
+// sphere of the box (more cells: fewer spheres per cell, more cell steps per ray).
+inline void build_grid_at(const lrt_sphere* s, int n, const std::vector<float4>& sph, float density, GridHost& G) {
     G = GridHost();
     G.count = n;
     std::vector<float> radii(n);
@@ -146,7 +141,7 @@ inline void build_grid_host(const lrt_sphere* s, int n, const std::vector<float4
         e3[k] = hi[k] - lo[k];
         vol *= e3[k];
     }
-    const double target = std::max(1.0, (double)grid_density() * (double)in.size());
+    const double target = std::max(1.0, (double)density * (double)in.size());
     float cell = (float)std::cbrt(vol / target);
     int nn[3];
     for (int k = 0; k < 3; ++k) nn[k] = std::max(1, std::min(512, (int)std::ceil(e3[k] / cell)));
@@ -207,6 +202,121 @@ inline void build_grid_host(const lrt_sphere* s, int n, const std::vector<float4
         G.max_refs = std::max(G.max_refs, r);
     }
     G.mean_refs = nonempty ? (double)G.rsph.size() / (double)nonempty : 0.0;
+}
+
+// The device's view of G (host arrays here: the host diagnostics and the resolution choice).
+inline GridView grid_view_host(const GridHost& G, const float4* all) {
+    GridView g;
+    g.cells = G.ranges.data();
+    g.rsph = G.rsph.data();
+    g.rid = G.rid.data();
+    g.bsph = G.bsph.data();
+    g.bid = G.bid.data();
+    g.all = all;
+    g.nbig = (int)G.bsph.size();
+    g.count = G.nx > 0 ? G.count : 0;
+    g.nx = G.nx;
+    g.ny = G.ny;
+    g.nz = G.nz;
+    g.lox = G.lo[0];
+    g.loy = G.lo[1];
+    g.loz = G.lo[2];
+    g.hx = G.h[0];
+    g.hy = G.h[1];
+    g.hz = G.h[2];
+    g.ihx = G.ih[0];
+    g.ihy = G.ih[1];
+    g.ihz = G.ih[2];
+    g.pad = G.pad;
+    g.errk = G.errk;
+    g.ext = G.ext;
+    g.on = 1;
+    return g;
+}
+
+// The walk's cost per ray for G, estimated on the host with the device's own walk: rays from
+// random points in the box in random directions (bounce and shadow rays) and from a shell
+// around it towards random points in it (camera rays); a sphere test counts 1, a cell step
+// kGridCellCost (its 8-byte load sits on the walk's critical path). Deterministic.
+#ifndef LRT_GRID_CELL_COST
+#define LRT_GRID_CELL_COST 1.5
+#endif
+constexpr double kGridCellCost = LRT_GRID_CELL_COST;
+inline double grid_cost(const GridHost& G, const std::vector<float4>& sph) {
+    if (G.nx == 0) return 0.0;
+    const GridView g = grid_view_host(G, sph.data());
+    uint32_t st = 0x9E3779B9u;
+    auto rnd = [&]() {   // xorshift32 in [0, 1)
+        st ^= st << 13;
+        st ^= st >> 17;
+        st ^= st << 5;
+        return (float)(st >> 8) * (1.0f / 16777216.0f);
+    };
+    const float hi[3] = {G.lo[0] + G.h[0] * G.nx, G.lo[1] + G.h[1] * G.ny, G.lo[2] + G.h[2] * G.nz};
+    float c[3], ext = 0.0f;
+    for (int k = 0; k < 3; ++k) {
+        c[k] = 0.5f * (G.lo[k] + hi[k]);
+        ext = std::max(ext, hi[k] - G.lo[k]);
+    }
+    double cost = 0.0;
+    const int m = 2048;
+    for (int i = 0; i < m; ++i) {
+        F3 o, t;
+        F3* pts[2] = {&o, &t};
+        for (int q = 0; q < 2; ++q) {
+            const float p3[3] = {G.lo[0] + rnd() * (hi[0] - G.lo[0]), G.lo[1] + rnd() * (hi[1] - G.lo[1]),
+                                 G.lo[2] + rnd() * (hi[2] - G.lo[2])};
+            *pts[q] = f3(p3[0], p3[1], p3[2]);
+        }
+        if (i & 1) {   // from a shell at 2x the box's extent towards a point in the box
+            F3 u = f3(rnd() - 0.5f, rnd() - 0.5f, rnd() - 0.5f);
+            const float l = std::sqrt(dot(u, u)) + 1e-6f;
+            o = f3(c[0], c[1], c[2]) + u * (2.0f * ext / l);
+        } else {       // from a point on a sphere of the grid, outwards (bounce and shadow rays)
+            const int id = G.rid.empty() ? 0 : G.rid[(size_t)(rnd() * (float)G.rid.size()) % G.rid.size()];
+            const float4 sp = sph[id];
+            F3 u = f3(rnd() - 0.5f, rnd() - 0.5f, rnd() - 0.5f);
+            const float l = std::sqrt(dot(u, u)) + 1e-6f;
+            u = u * (1.0f / l);
+            o = f3(sp.x, sp.y, sp.z) + u * std::sqrt(sp.w);
+            F3 v = f3(rnd() - 0.5f, rnd() - 0.5f, rnd() - 0.5f);
+            if (dot(v, u) < 0.0f) v = -v;
+            t = o + v;
+        }
+        const Ray r = make_ray(o, t - o);
+        GridStats gs;
+        float tt;
+        (void)ClosestHitGrid(r.orig, r.dir, g, tt, &gs);
+        cost += gs.spheres + kGridCellCost * gs.cells;
+    }
+    return cost / m;
+}
+
+// The grid at the resolution of lowest estimated cost among a few densities (cells per
+// sphere): how the cells fall against the spheres' own spacing matters as much as their
+// number. On config 4's field (a jittered 36 x 28 lattice of spheres) the model picks 36 x 1 x
+// 29 cells, one lattice site each: 2.6-2.9 sphere tests per ray against 4.1-4.6 at density 2
+// (tools/accel_stats.py); measured densities 0.5-2 ran 163-185 ms (profiles/r4_e, r4_f).
+// LRT_GRID_DENSITY fixes one instead.
+inline void build_grid_host(const lrt_sphere* s, int n, const std::vector<float4>& sph, GridHost& G) {
+    if (const char* e = getenv("LRT_GRID_DENSITY")) {
+        const float v = (float)atof(e);
+        build_grid_at(s, n, sph, v > 0.05f && v < 64.0f ? v : 1.0f, G);
+        return;
+    }
+    double best = 0.0;
+    bool have = false;
+    for (float dens : {0.5f, 0.6f, 0.75f, 0.9f, 1.0f, 1.25f, 1.5f, 2.0f, 3.0f}) {
+        GridHost T;
+        build_grid_at(s, n, sph, dens, T);
+        const double c = grid_cost(T, sph);
+        if (!have || c < best) {
+            best = c;
+            have = true;
+            G = std::move(T);
+        }
+        if (T.nx == 0 && have) break;   // no walk at all: every density is the same
+    }
 }
 
 // The scene gets the grid when its spheres spread evenly enough: few spheres per cell and

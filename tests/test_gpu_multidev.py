@@ -262,11 +262,13 @@ def test_new_view_borrows_order_bitwise(gpu):
     order (order=3) instead of running in queue order; the pixels are the new view's."""
     from learnraytracing_amd import _lib as L
     w, h = 1280, 720
+    # (flags 512: the pool kernel; a host buffer of <= 4 frames otherwise takes the pipelined
+    # host path, whose colours v0 renders)
     for _ in range(2):   # view A: recording launch, then its own order
-        _host(gpu, gpu.Job(width=w, height=h, frames=4, max_depth=8))
+        _host(gpu, gpu.Job(width=w, height=h, frames=4, max_depth=8, flags=512))
     assert L.last_launch()["order"] == "2"
     cam = gpu.make_camera((0.3, 2.1, 3), (0, 0, 0), (0, 1, 0), 60, w / h, 0.1, 3)
-    buf, rays = _host(gpu, gpu.Job(width=w, height=h, frames=4, max_depth=8, camera=cam))
+    buf, rays = _host(gpu, gpu.Job(width=w, height=h, frames=4, max_depth=8, camera=cam, flags=512))
     assert L.last_launch()["order"] == "3"
     want, wrays = oracle.orc_render(w, h, 4, 8, cam22=cam.to22())
     _bitwise(buf, want, "moved camera, borrowed order")
