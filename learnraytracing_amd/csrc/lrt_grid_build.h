@@ -321,6 +321,10 @@ inline void build_grid_host(const lrt_sphere* s, int n, const std::vector<float4
 
 // The scene gets the grid when its spheres spread evenly enough: few spheres per cell and
 // few tested by every ray (LRT_ACCEL=bvh | grid forces one).
+inline bool grid_forced() {
+    const char* e = getenv("LRT_ACCEL");
+    return e && std::string(e) == "grid";
+}
 inline bool grid_suitable(const GridHost& G) {
     const char* e = getenv("LRT_ACCEL");
     if (e && std::string(e) == "bvh") return false;

@@ -10,13 +10,13 @@ template <int MAXD, int kPix>
 int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     constexpr int TX = PoolTile<kPix>::X, TY = PoolTile<kPix>::Y;
     const long long ntiles = (long long)((xc + TX - 1) / TX) * ((rows + TY - 1) / TY);
-    const size_t stack = sizeof(float4) * kTraceLdsLevels * 64 + kPowTableBytes + (a.bv.on ? 0 : kRenormBytes);
+    const int acc = a.gv.on ? kAccGrid : a.bv.on ? kAccBvh : kAccScan;
+    const size_t stack = sizeof(float4) * kTraceLdsLevels * 64 + kPowTableBytes + (acc ? 0 : kRenormBytes);
     const size_t scene = lds ? sizeof(float4) * (4 * (size_t)a.count + (size_t)(a.nlights + 3) / 4 + 1) : 0;
     a.bvh_stack_offset = (int)(stack + scene);
-    const int acc = a.gv.on ? kAccGrid : a.bv.on ? kAccBvh : kAccScan;
     const size_t bstk = acc == kAccBvh ? sizeof(unsigned short) * ctx().bvh_stack_levels * 64 : 0;
     const size_t ldsb = stack + scene + bstk;
-    const bool fixed = lds && !a.bv.on && a.count == kFixedSpheres;
+    const bool fixed = lds && acc == kAccScan && a.count == kFixedSpheres;
     const void* kern = acc == kAccGrid ? (lds ? (const void*)pool_kernel<MAXD, true, kAccGrid, kPix>
                                               : (const void*)pool_kernel<MAXD, false, kAccGrid, kPix>)
                        : acc == kAccBvh ? (lds ? (const void*)pool_kernel<MAXD, true, kAccBvh, kPix>

@@ -324,7 +324,7 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     // the uniform grid where the scene suits it (grid_suitable; LRT_F_BVH / LRT_F_GRID force
     // one), except for feature launches (v0's BVH instances)
     a.gv = ctx().gv;
-    a.gv.on = (a.bv.on && ctx().gv.on && !want_feat && !(d->flags & LRT_F_BVH) &&
+    a.gv.on = (ctx().gv.on && !(d->flags & LRT_F_NO_BVH) && !want_feat && !(d->flags & LRT_F_BVH) &&
                (ctx().grid_pick || (d->flags & LRT_F_GRID)))
                   ? 1
                   : 0;
@@ -347,7 +347,7 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     if (frame && (want_feat || colours_out))
         return fail(LRT_E_INVALID, "a frame destination is for plain renders (no features, no colours-only)");
     if (colours_out) {   // v0, one frame lane per pixel, sample mode
-        if (want_feat || !lds || a.bv.on) return fail(LRT_E_INVALID, "colours-only render: LDS linear-scan scenes only");
+        if (want_feat || !lds || a.bv.on || a.gv.on) return fail(LRT_E_INVALID, "colours-only render: LDS linear-scan scenes only");
         if (d->max_depth <= 8) return launch_v0_d8(a, lds, d->x_count, d->row_count, d->frames, false, true, s);
         return launch_v0_d64(a, lds, d->x_count, d->row_count, d->frames, false, true, s);
     }
@@ -375,7 +375,7 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
 // frames, a GPU's row shard, take v0's frame lanes and sample mode; features are v0's).
 int auto_kernel(const KernelArgs& a, const lrt_render_desc* d, bool feat) {
     if (feat || d->frames < 4) return LRT_F_SIMPLE;
-    if (!(a.bv.on || d->max_depth > 8) && !pool_order_on()) return LRT_F_SIMPLE;
+    if (!(a.bv.on || a.gv.on || d->max_depth > 8) && !pool_order_on()) return LRT_F_SIMPLE;
     const int pix = pool_pixels(d->frames, d->x_count, d->row_count);
     const long long tiles = pool_tiles(pix, d->x_count, d->row_count);
     const long long slots = 16LL * ctx().num_cus;   // resident waves (4 per SIMD)

@@ -338,9 +338,11 @@ int upload_scene(Context& c, const lrt_sphere* s, const lrt_material* m, int n) 
         // the LDS traversal stack is sized to B.stack_levels entries per lane, which bounds
         // every push (StackPush: at most one entry per level above the current node)
         if (B.stack_levels > kBvhStackLevels) return fail(LRT_E_INVALID, "BVH deeper than the traversal stack");
-        build_grid_host(s, n, sph, G);
         if (B.nodes.empty()) B.nodes.assign(4, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     }
+    // the grid for every scene: the default above kBvhMinSpheres where it suits the scene,
+    // opt-in below (LRT_F_GRID, LRT_ACCEL=grid)
+    if (n > 0) build_grid_host(s, n, sph, G);
     free_scene(c);
     LRT_HIP(upload(c.d_sph, sph));
     LRT_HIP(upload(c.d_mats, mats));
@@ -355,6 +357,8 @@ int upload_scene(Context& c, const lrt_sphere* s, const lrt_material* m, int n) 
         c.bvh_margin = B.margin;
         c.bvh_stack_levels = B.stack_levels;
         c.bvh_on = 1;
+    }
+    if (n > 0) {
         LRT_HIP(upload(c.d_grid_cells, G.ranges));
         LRT_HIP(upload(c.d_grid_rsph, G.rsph));
         LRT_HIP(upload(c.d_grid_rid, G.rid));
@@ -385,7 +389,7 @@ int upload_scene(Context& c, const lrt_sphere* s, const lrt_material* m, int n) 
         g.errk = G.errk;
         g.ext = G.ext;
         g.on = 1;
-        c.grid_pick = grid_suitable(G);
+        c.grid_pick = accel ? grid_suitable(G) : grid_forced();
     }
     c.count = n;
     ++c.scene_version;

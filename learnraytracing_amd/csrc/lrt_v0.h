@@ -274,16 +274,16 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     constexpr int kTileRows = kBlockWavesY * (64 / kSplit / WaveCols(kSplit));
     constexpr int kTileX = WaveCols(kSplit) * kBlockWavesX;
     const long long ntiles = (long long)((xc + kTileX - 1) / kTileX) * ((rows + kTileRows - 1) / kTileRows);
-    const size_t stack = sizeof(float4) * kTraceLdsLevels * kBlock + kPowTableBytes + (a.bv.on ? 0 : kRenormBytes);
+    const int acc = a.gv.on ? kAccGrid : a.bv.on ? kAccBvh : kAccScan;
+    const size_t stack = sizeof(float4) * kTraceLdsLevels * kBlock + kPowTableBytes + (acc ? 0 : kRenormBytes);
     const size_t scene = lds ? sizeof(float4) * (4 * (size_t)a.count + (size_t)(a.nlights + 3) / 4 + 1) : 0;
     a.bvh_stack_offset = (int)(stack + scene);
     // v0 sizes the LDS traversal stack to this scene's BVH depth (1000 spheres: ~9
     // levels, 1.2 KB instead of 3 KB per wave -- the difference between 13 and 16 waves/CU)
-    const int acc = a.gv.on ? kAccGrid : a.bv.on ? kAccBvh : kAccScan;
     const size_t bstk = acc == kAccBvh ? sizeof(unsigned short) * ctx().bvh_stack_levels * kBlock : 0;
     const size_t ldsb = stack + (lds ? scene : 0) + bstk;
     // the reference's own scene size (parallel.cpp:27) gets the unrolled-scan instances
-    const bool fixed = lds && !a.bv.on && a.count == kFixedSpheres;
+    const bool fixed = lds && acc == kAccScan && a.count == kFixedSpheres;
     const void* kern = acc == kAccGrid ? (lds ? (const void*)trace_kernel<MAXD, true, kAccGrid, kSplit, kFeat>
                                               : (const void*)trace_kernel<MAXD, false, kAccGrid, kSplit, kFeat>)
                        : acc == kAccBvh ? (lds ? (const void*)trace_kernel<MAXD, true, kAccBvh, kSplit, kFeat>
@@ -307,7 +307,7 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     const int rounds = (a.frames + kSplit - 1) / kSplit;
     const size_t npix = (size_t)xc * rows;
     bool samp = false;
-    if constexpr (!kFeat && kSplit == 1) samp = a.sampOnly && lds && !a.bv.on;
+    if constexpr (!kFeat && kSplit == 1) samp = a.sampOnly && lds && acc == kAccScan;
     if constexpr (!kFeat && kSplit >= 4) {
         static int mode = -1;
         if (mode < 0) {
@@ -315,7 +315,7 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
             mode = v ? atoi(v) : 1;
         }
         const long long slots = (long long)per_cu * cus;
-        samp = mode > 0 && lds && !a.bv.on && rounds >= 2 && npix * (size_t)a.frames * sizeof(float4) <= (2ull << 30) &&
+        samp = mode > 0 && lds && acc == kAccScan && rounds >= 2 && npix * (size_t)a.frames * sizeof(float4) <= (2ull << 30) &&
                (mode == 2 || ntiles < 16 * slots);
     }
     if (a.sampOnly && !samp) return fail(LRT_E_INVALID, "colours-only render: needs the LDS linear scan, one frame lane");

@@ -526,3 +526,39 @@ def test_non_finite_prev_propagates_like_reference(gpu, f0, frames):
     assert same.all(), f"{int((~same).sum())} channels differ"
     assert np.isnan(g).sum() >= int(np.isnan(init[..., :3]).sum())
     assert np.array_equal(got[..., 3].view(np.uint32), init[..., 3].view(np.uint32))
+
+
+GRID = 2048   # LRT_F_GRID: the uniform grid, also for scenes the policy leaves on the linear scan
+
+
+@pytest.mark.parametrize("kflags", [V0, POOL], ids=["v0", "pool"])
+def test_grid_on_small_scenes_vs_oracle(gpu, manifest, images, kflags):
+    """The grid forced on the reference's own 9 spheres (configs 1-3) and the fuzzed scenes
+    (9 spheres each, 1-3 lights, every material): the same bits as the scan's goldens."""
+    from learnraytracing_amd import _lib as L
+    from learnraytracing_amd.scene import scene_from_arrays
+    buf, rays = _render(gpu, 1280, 720, 4, 8, flags=kflags | GRID)
+    info = L.last_launch()
+    assert info["acc"] == "grid", info
+    want, wrays = oracle.orc_render(1280, 720, 4, 8)
+    _assert_bitwise(buf, want[..., :3], f"flags={kflags | GRID} config2 full frame")
+    assert rays == wrays
+    buf, rays = _render(gpu, 1920, 1080, 16, 50, y0=520, yc=24, flags=kflags | GRID)
+    want, wrays = oracle.orc_render(1920, 1080, 16, 50, y0=520, yc=24)
+    _assert_bitwise(buf, want[..., :3], f"flags={kflags | GRID} config3 band")
+    assert rays == wrays
+    try:
+        for fz in manifest["fuzz"]:
+            gpu.set_scene(*scene_from_arrays(fz["spheres"], fz["mats"]))
+            cam = L.Camera()
+            vals = fz["camera"]
+            names = ("origin", "a", "u", "r", "lowerLeftCorner", "horizontalVec", "verticalVec")
+            for i, n in enumerate(names):
+                setattr(cam, n, L.f3(*vals[3 * i:3 * i + 3]))
+            cam.lensRadius = vals[21]
+            buf, rays = _render(gpu, fz["w"], fz["h"], fz["frames"], fz["max_depth"], camera=cam,
+                                flags=kflags | GRID)
+            _assert_bitwise(buf, images[fz["name"]], f"flags={kflags | GRID} " + fz["name"])
+            assert rays == fz["rays"], fz["name"]
+    finally:
+        gpu.set_scene(*gpu.default_scene())
