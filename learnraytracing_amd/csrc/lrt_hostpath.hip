@@ -126,7 +126,9 @@ bool host_pipeline(const lrt_render_desc* d, size_t bytes) {
         const char* e = getenv("LRT_HOST_PIPELINE");
         return e ? atoi(e) : 1;
     }();
-    const bool bvh = ctx().bvh_on && !(d->flags & LRT_F_NO_BVH);
+    // (an accelerated scene: the BVH, or the grid where render_device would pick it)
+    const bool bvh = !(d->flags & LRT_F_NO_BVH) &&
+                     (ctx().bvh_on || (ctx().gv.on && (ctx().grid_pick || (d->flags & LRT_F_GRID))));
     const bool lds = !(d->flags & LRT_F_SCENE_GLOBAL) &&
                      sizeof(float4) * (kTraceLdsLevels * kBlock + 4 * (size_t)ctx().count + ctx().nlights / 4 + 1) <=
                          64 * 1024;

@@ -13,6 +13,9 @@ import learnraytracing_amd as lrt
 
 w, h, frames = 1280, 720, int(sys.argv[1]) if len(sys.argv) > 1 else 30
 pinned = len(sys.argv) > 2 and sys.argv[2] == "pinned"
+if "torch" in sys.argv[2:]:   # as bench.py's process: torch imported, its HIP context up
+    import torch
+    torch.zeros(1, device="cuda").sum().item()
 lrt.InitializeTest()
 bb = lrt.pinned_backbuffer(w * h * 4) if pinned else np.zeros(w * h * 4, np.float32)
 lrt.DrawTest(0.0, 0, w, h, bb)  # warm-up

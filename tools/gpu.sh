@@ -9,7 +9,7 @@
 #   bench=C[,ARGS]    bench.py --config C (ARGS: extra bench flags, ';'-separated)
 #   trace=C[,ARGS]    rocprofv3 --kernel-trace --stats of bench.py --config C --streams 1
 #   pmc=C,GROUP[,ARGS] one rocprofv3 --pmc pass (GROUP: fetch | write | sq | sq2 | cache) of bench --config C
-#   py=SCRIPT[,ARGS]  python SCRIPT ARGS (diagnostics under tools/)
+#   py=SCRIPT[,ARGS]  python SCRIPT ARGS (diagnostics under tools/; NAME=VALUE tokens set the environment)
 #   ab=V,C[,ARGS]     bench.py --config C with LRT_LIB=build_exp/liblrt_V.so (tools/build_variant.sh),
 #                     timed region only (A/B of library variants; V=default: the in-tree library;
 #                     NAME=VALUE tokens in ARGS set environment variables)
@@ -63,7 +63,11 @@ for s in "$@"; do
            [[ "$rest" == *,* ]] && pextra=${rest#*,}
            run "pmc_c${c}_$g" 300 rocprofv3 --pmc ${PMC[$g]} -d "$out" -o "pmc_c${c}_$g" --output-format csv -- \
              python3 bench.py --config "$c" --steps 2 --warmup 1 --streams 1 --no-cpu-baseline --no-extra-legs ${pextra//;/ } ;;
-    py)    run "py$i" 600 python ${val//,/ } ;;
+    py)    penv=() pargs=()   # NAME=VALUE tokens are environment settings (e.g. LRT_LIB=...)
+           for tok in ${val//,/ }; do
+             if [[ "$tok" =~ ^[A-Z_][A-Z0-9_]*= ]]; then penv+=("$tok"); else pargs+=("$tok"); fi
+           done
+           run "py$i" 600 env "${penv[@]}" python "${pargs[@]}" ;;
     ab)    c2=${rest%%,*}
            extra2=""
            [[ "$rest" == *,* ]] && extra2=${rest#*,}
