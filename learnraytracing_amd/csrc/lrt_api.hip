@@ -27,7 +27,27 @@ int hip_fail(hipError_t e, const char* what) {
 int init_context(Context& c, int dev) {
     c = Context();
     c.device = dev;
-    LRT_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    LRT_HIP(hipDeviceGetAttribute(&c.num_cus, hipDeviceAttributeMultiprocessorCount, dev));
+    // The context's streams are created together, first, the render stream at high priority.
+    // HIP deals a process's streams to a few hardware queues (GPU_MAX_HW_QUEUES = 4), and
+    // DrawTest's lerps (stream), copies (s_in) and look-ahead render (a CU-masked stream) must
+    // not queue behind one another: created lazily, between other streams, they did on some
+    // offsets -- a pageable DrawTest at 1280x720 took 0.67-0.77 ms/frame instead of 0.49-0.52
+    // (tools/drawtest_queues.py, profiles/r4_m); a high-priority queue is one no stream of normal
+    // priority shares. LRT_STREAM_PRIO: 1 (default) as described, 0 all at normal priority.
+    {
+        static const int prio_mode = [] {
+            const char* e = getenv("LRT_STREAM_PRIO");
+            return e ? atoi(e) : 1;
+        }();
+        int least = 0, greatest = 0;
+        LRT_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        LRT_HIP(hipStreamCreateWithPriority(&c.stream, hipStreamNonBlocking, prio_mode >= 1 ? greatest : least));
+        LRT_HIP(hipStreamCreateWithPriority(&c.s_in, hipStreamNonBlocking, least));
+    }
+    if (int rc = create_lookahead_stream(c)) return rc;
+    for (int k = 0; k < Context::kHostChunks; ++k) LRT_HIP(hipEventCreateWithFlags(&c.ev_in[k], hipEventDisableTiming));
+    LRT_HIP(hipEventCreateWithFlags(&c.ev_ret, hipEventDisableTiming));
     LRT_HIP(hipMalloc(&c.d_rays, sizeof(unsigned long long)));
     LRT_HIP(hipHostMalloc((void**)&c.h_rays, sizeof(unsigned long long), hipHostMallocDefault));
     LRT_HIP(hipMalloc(&c.d_tiles, sizeof(unsigned long long) * kQueueSlots * kTileSetU64));
@@ -38,7 +58,6 @@ int init_context(Context& c, int dev) {
         LRT_HIP(hipMalloc(&c.d_lerp, sizeof(float) * kLerpTable));
         LRT_HIP(hipMemcpy(c.d_lerp, t.data(), sizeof(float) * kLerpTable, hipMemcpyHostToDevice));
     }
-    LRT_HIP(hipDeviceGetAttribute(&c.num_cus, hipDeviceAttributeMultiprocessorCount, dev));
     {   // keep freed stream-ordered blocks (the per-launch path-stack overflow) in the
         // pool instead of returning them to the driver at every synchronisation
         hipMemPool_t pool;

@@ -179,6 +179,21 @@ int lookahead_reserved_cus() {
     return k;
 }
 
+// The look-ahead's CU-masked stream and events (init_context creates them beside the context's
+// other streams, so that each has a hardware queue of its own).
+int create_lookahead_stream(Context& c) {
+    Context::Lookahead& la = c.ahead;
+    if (la.stream || !draw_lookahead_on()) return LRT_OK;
+    const int n = c.num_cus, keep = std::max(1, n - std::max(0, lookahead_reserved_cus()));
+    std::vector<uint32_t> mask((size_t)(n + 31) / 32, 0u);
+    for (int k = 0; k < keep; ++k) mask[k / 32] |= 1u << (k % 32);   // spread over XCDs (k % 8)
+    LRT_HIP(hipExtStreamCreateWithCUMask(&la.stream, (uint32_t)mask.size(), mask.data()));
+    c.masked_streams.emplace_back(la.stream, keep);
+    LRT_HIP(hipEventCreateWithFlags(&la.ev, hipEventDisableTiming));
+    LRT_HIP(hipEventCreateWithFlags(&la.ev_render, hipEventDisableTiming));
+    return LRT_OK;
+}
+
 // The lerp grid: a few blocks per CU, each striding over the chunk (posted PCIe writes need
 // no more in flight; a full grid would wait for CUs behind the look-ahead render)
 unsigned merge_blocks(size_t n) {
@@ -239,16 +254,7 @@ int render_host_pipelined(const lrt_render_desc* d, float* buf, float* hdev, siz
         const int nx = hit ? la.cur ^ 1 : la.cur;
         lrt_render_desc nd = *d;
         nd.frame0 = d->frame0 + 1;
-        bool ok = true;
-        if (!la.stream) {
-            const int n = ctx().num_cus, keep = std::max(1, n - std::max(0, lookahead_reserved_cus()));
-            std::vector<uint32_t> mask((size_t)(n + 31) / 32, 0u);
-            for (int c = 0; c < keep; ++c) mask[c / 32] |= 1u << (c % 32);   // spread over XCDs (c % 8)
-            ok = hipExtStreamCreateWithCUMask(&la.stream, (uint32_t)mask.size(), mask.data()) == hipSuccess &&
-                 hipEventCreateWithFlags(&la.ev, hipEventDisableTiming) == hipSuccess &&
-                 hipEventCreateWithFlags(&la.ev_render, hipEventDisableTiming) == hipSuccess;
-            if (ok) ctx().masked_streams.emplace_back(la.stream, keep);
-        }
+        bool ok = la.stream || create_lookahead_stream(ctx()) == LRT_OK;
         if (ok && la.bytes[nx] < cbytes) {
             if (la.col[nx]) (void)hipFree(la.col[nx]);
             la.col[nx] = nullptr;

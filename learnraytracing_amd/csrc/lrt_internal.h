@@ -380,6 +380,7 @@ hipError_t fill_iota(int* v, int n, hipStream_t s);
 int ensure_frame(size_t bytes);
 float* host_pinned(float* buf);
 // drawtest: the reference API's call (lrt_draw_test: the look-ahead render)
+int create_lookahead_stream(Context& c);
 int render_host(const lrt_render_desc* d, float* buf, long long* out_rays, const lrt_features* feat = nullptr,
                 bool drawtest = false);
 

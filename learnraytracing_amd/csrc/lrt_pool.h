@@ -53,6 +53,23 @@ typedef const KernelArgs* KArgPtr;
 __device__ __forceinline__ KArgPtr opaque_args() { return nullptr; }
 #endif
 
+// The grid's spheres tested first by every query (the ground, the light: GridStart) are read
+// from an LDS copy (at a.bvh_stack_offset: the grid has no traversal stack) instead of through
+// L1/L2, and their uniform loads leave the walk's latency chain (LRT_GRID_BIG_LDS).
+#ifndef LRT_GRID_BIG_LDS
+#define LRT_GRID_BIG_LDS 1
+#endif
+template <int kAcc>
+__device__ __forceinline__ GridView pool_grid_view(float4* smem) {
+    GridView g = opaque_args()->gv;
+    if (LRT_GRID_BIG_LDS) {
+        float4* b = reinterpret_cast<float4*>(reinterpret_cast<char*>(smem) + opaque_args()->bvh_stack_offset);
+        g.bsph = b;
+        g.bid = reinterpret_cast<const int*>(b + g.nbig);
+    }
+    return g;
+}
+
 #ifndef LRT_POOL_OVF_ZERO
 #define LRT_POOL_OVF_ZERO 1
 #endif
@@ -87,6 +104,13 @@ __global__ __launch_bounds__(64, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0
         for (int i = lane; i < a.count; i += 64) s_sph[i] = a.sph[i];
         for (int i = lane; i < 3 * a.count; i += 64) s_mat[i] = a.mats[i];
         for (int i = lane; i < a.nlights; i += 64) s_lights[i] = a.lights[i];
+    }
+    if (kAcc == kAccGrid && LRT_GRID_BIG_LDS) {   // (pool_grid_view)
+        float4* b = reinterpret_cast<float4*>(reinterpret_cast<char*>(smem) + a.bvh_stack_offset);
+        for (int i = lane; i < a.gv.nbig; i += 64) {
+            b[i] = a.gv.bsph[i];
+            reinterpret_cast<int*>(b + a.gv.nbig)[i] = a.gv.bid[i];
+        }
     }
     __syncthreads();
     SceneView sc;
@@ -264,7 +288,7 @@ __global__ __launch_bounds__(64, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0
                     const bool hasS = pend && dl.on;
                     if constexpr (kAcc == kAccGrid) {
                         const float4 ls = hasS ? sc.sph[dl.li] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                        const GridView gv = opaque_args()->gv;
+                        const GridView gv = pool_grid_view<kAcc>(smem);
                         nid = ClosestHitDualGrid(r.orig, r.dir, hasS, dl.l, dl.li, ls, gv, nt, lit);
                     } else if constexpr (kAcc == kAccBvh) {
                         if (coherent) {
@@ -303,7 +327,7 @@ __global__ __launch_bounds__(64, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0
                         if (depth < a.maxDepth) {
                             F3 lightE;
                             dl.on = false;
-                            if constexpr (kAcc == kAccGrid) sc.gv = opaque_args()->gv;   // other lights' shadow rays
+                            if constexpr (kAcc == kAccGrid) sc.gv = pool_grid_view<kAcc>(smem);   // other lights' shadow rays
                             const F3 X = ScatterDir<kAcc, kNS>(mat, nid, r, rec, lightE, rays, rng, sc, &dl, coherent);
                             sec_count(sc, kSecPost);
                             const F3 dir = renormalize(normalize(X), sc.rnlut);   // Ray(rec.pos, normalize(X))

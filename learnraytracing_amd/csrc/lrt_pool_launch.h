@@ -14,7 +14,9 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     const size_t stack = sizeof(float4) * kTraceLdsLevels * 64 + kPowTableBytes + (acc ? 0 : kRenormBytes);
     const size_t scene = lds ? sizeof(float4) * (4 * (size_t)a.count + (size_t)(a.nlights + 3) / 4 + 1) : 0;
     a.bvh_stack_offset = (int)(stack + scene);
-    const size_t bstk = acc == kAccBvh ? sizeof(unsigned short) * ctx().bvh_stack_levels * 64 : 0;
+    // the BVH's traversal stack, or the grid's first-tested spheres (pool_grid_view)
+    const size_t bstk = acc == kAccBvh ? sizeof(unsigned short) * ctx().bvh_stack_levels * 64
+                        : acc == kAccGrid ? (sizeof(float4) + sizeof(int)) * (size_t)a.gv.nbig : 0;
     const size_t ldsb = stack + scene + bstk;
     const bool fixed = lds && acc == kAccScan && a.count == kFixedSpheres;
     const void* kern = acc == kAccGrid ? (lds ? (const void*)pool_kernel<MAXD, true, kAccGrid, kPix>

@@ -11,6 +11,7 @@ import torch
 
 sys.path.insert(0, ".")
 import learnraytracing_amd as lrt  # noqa: E402
+from learnraytracing_amd import _lib as L  # noqa: E402
 
 W, H, N = 1280, 720, int(sys.argv[1]) if len(sys.argv) > 1 else 200
 torch.cuda.set_device(0)
@@ -29,7 +30,7 @@ def rate(what):
         lrt.DrawTest(0.0, frame[0], W, H, bb)
         frame[0] += 1
     dt = (time.perf_counter() - t0) / N
-    print(f"{what:48s} {dt * 1e3:.4f} ms/frame  {lrt.last_launch().get('host')}", flush=True)
+    print(f"{what:48s} {dt * 1e3:.4f} ms/frame  {L.last_launch().get('host')}", flush=True)
 
 
 rate("alone")
@@ -52,4 +53,13 @@ rate("after a scene upload")
 del host
 torch.cuda.synchronize()
 rate("after freeing the pinned buffers")
+lrt.ShutdownTest()
+
+# bench.py's own leg, in this process (its numbers are the bench line's)
+import bench  # noqa: E402
+
+lrt.InitializeTest()
+for k in range(2):
+    print("bench.drawtest_leg", bench.drawtest_leg(lrt)["ms_per_frame"], flush=True)
+rate("rate() after the bench leg")
 lrt.ShutdownTest()
