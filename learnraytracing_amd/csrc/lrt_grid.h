@@ -43,7 +43,24 @@ struct GridView {
     float errk;              // a ray may walk if 2^-16 (max|o| + ext) < errk (= pad / 2)
     float ext;               // max |coordinate| of the box
     int on;
+    unsigned cells_refs;     // entries of rsph / rid (the LDS copy's size, LRT_POOL_GRID_WPB)
 };
+
+// The walk's reads of the cell ranges and the cell-ordered spheres. kL = 1: the pool kernel's
+// block-shared LDS copy (LRT_POOL_GRID_WPB): the view's pointers are generic addresses of
+// that copy, read here as LDS (ds_read instead of flat loads). Any other reader of the same
+// view (the other lights' shadow queries) goes through the generic pointers.
+template <class T>
+LRT_DEV T grid_ld(const T* p, unsigned i, std::integral_constant<int, 1>) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return ((const __attribute__((address_space(3))) T*)p)[i];
+#else
+    return p[i];   // (the host pass only parses the kernels)
+#endif
+}
+template <class T>
+LRT_DEV T grid_ld(const T* p, unsigned i, std::integral_constant<int, 0>) { return p[i]; }
+#define LRT_GRID_LD(kL, p, i) grid_ld((p), (unsigned)(i), std::integral_constant<int, (kL)>())
 
 // Host diagnostics (lrt_grid_stats): cell steps, sphere tests and fallback scans.
 struct GridStats { int cells = 0, spheres = 0, fallback = 0; };
@@ -87,6 +104,7 @@ LRT_DEV void GridTest(GridQuery& q, const float4& s, int id) {
 
 // Starts q's walk along q.d (q.bestT / q.best / q.li set by the caller): the big spheres,
 // then the cell where the ray enters the box.
+template <int kL = 0>
 LRT_DEV void GridStart(GridQuery& q, const GridView& g, GridStats* st = nullptr) {
     // (a shadow query skips its own light: the light's candidate IS the bar, and a tie with the
     // same index changes nothing -- GridBeats is false for it)
@@ -140,7 +158,7 @@ LRT_DEV void GridStart(GridQuery& q, const GridView& g, GridStats* st = nullptr)
             : q.d.y < 0.0f ? (GridPlane(g.loy, q.cy, g.hy) - q.o.y) * q.inv.y : __builtin_inff();
     q.tnz = q.d.z > 0.0f ? (GridPlane(g.loz, q.cz + 1, g.hz) - q.o.z) * q.inv.z
             : q.d.z < 0.0f ? (GridPlane(g.loz, q.cz, g.hz) - q.o.z) * q.inv.z : __builtin_inff();
-    const uint2 cr = g.cells[(unsigned)((q.cz * g.ny + q.cy) * g.nx + q.cx)];
+    const uint2 cr = LRT_GRID_LD(kL, g.cells, (q.cz * g.ny + q.cy) * g.nx + q.cx);
     q.j = cr.x;
     q.jend = cr.y;
     q.mode = 0;
@@ -151,6 +169,7 @@ LRT_DEV void GridStart(GridQuery& q, const GridView& g, GridStats* st = nullptr)
 // walk), then one sphere test. The step is straight-line code: the axis with the nearest
 // plane (x, then y, then z on ties) is selected rather than branched on, so a wave whose
 // lanes step along different axes issues one sequence, not three.
+template <int kL>
 LRT_DEV void GridAdvance(GridQuery& q, const GridView& g, GridStats* st) {
     if (q.mode != 0 || q.j < q.jend) return;
     const float T = __builtin_fminf(__builtin_fminf(q.tnx, q.tny), q.tnz);
@@ -175,7 +194,7 @@ LRT_DEV void GridAdvance(GridQuery& q, const GridView& g, GridStats* st) {
     q.tnx = ax ? (GridPlane(g.lox, q.cx + ux, g.hx) - q.o.x) * q.inv.x : q.tnx;
     q.tny = ay ? (GridPlane(g.loy, q.cy + uy, g.hy) - q.o.y) * q.inv.y : q.tny;
     q.tnz = az ? (GridPlane(g.loz, q.cz + uz, g.hz) - q.o.z) * q.inv.z : q.tnz;
-    const uint2 cr = g.cells[(unsigned)((q.cz * g.ny + q.cy) * g.nx + q.cx)];   // one 8-byte load per cell
+    const uint2 cr = LRT_GRID_LD(kL, g.cells, (q.cz * g.ny + q.cy) * g.nx + q.cx);   // one 8-byte load per cell
     q.j = cr.x;
     q.jend = cr.y;
     if (st) st->cells += 1;
@@ -183,17 +202,18 @@ LRT_DEV void GridAdvance(GridQuery& q, const GridView& g, GridStats* st) {
 // The fallback (mode 1, never in practice: origins ~8 scene sizes away) runs through the same
 // sphere test over the whole scene in index order (the reference's own scan, index = position):
 // one copy of the test in the loop.
+template <int kL = 0>
 LRT_DEV void GridIter(GridQuery& q, const GridView& g, GridStats* st) {
-    GridAdvance(q, g, st);
+    GridAdvance<kL>(q, g, st);
     if (q.mode != 2 && q.j < q.jend) {
         if (st) st->spheres += 1;
         const unsigned j = q.j++;
         const bool scan = q.mode == 1;
-        const float4 s = (scan ? g.all : g.rsph)[j];
+        const float4 s = scan ? g.all[j] : LRT_GRID_LD(kL, g.rsph, j);
         const float cand = GridCand(q.o, q.d, s);
         // the original index is read only when it can matter (a win or an exact tie)
         if (cand < q.bestT || (cand == q.bestT && q.best != -1)) {
-            const int id = scan ? (int)j : g.rid[j];
+            const int id = scan ? (int)j : LRT_GRID_LD(kL, g.rid, j);
             if (GridBeats(q, cand, id)) {
                 q.bestT = cand;
                 q.best = id;
@@ -237,6 +257,7 @@ LRT_DEV bool ShadowReachesLightGrid(const F3& o, const F3& d, int li, const floa
 
 // The pool kernel's two queries from one origin in one loop (as ClosestHitDualBVH4): the
 // deferred shadow ray of the last light (when hasS), then the bounce ray's closest hit.
+template <int kL = 0>
 LRT_DEV void GridDualInit(GridQuery& q, const F3& o, const F3& db, bool hasS, const F3& ds, int li,
                           const float4& lightSph, const GridView& g, GridStats* st) {
     q.o = o;
@@ -249,10 +270,11 @@ LRT_DEV void GridDualInit(GridQuery& q, const F3& o, const F3& db, bool hasS, co
     q.d = q.sh ? ds : db;
     q.bestT = q.sh ? candL : kMaxT;
     q.best = q.sh ? -2 : -1;
-    GridStart(q, g, st);
+    GridStart<kL>(q, g, st);
 }
+template <int kL = 0>
 LRT_DEV void GridDualStep(GridQuery& q, const GridView& g, GridStats* st) {
-    GridIter(q, g, st);
+    GridIter<kL>(q, g, st);
     const bool qdone = q.mode == 2 || (q.sh && q.best != -2);
     if (qdone) {
         if (q.sh) {
@@ -261,17 +283,18 @@ LRT_DEV void GridDualStep(GridQuery& q, const GridView& g, GridStats* st) {
             q.d = q.db;
             q.bestT = kMaxT;
             q.best = -1;
-            GridStart(q, g, st);
+            GridStart<kL>(q, g, st);
         } else {
             q.busy = false;
         }
     }
 }
+template <int kL = 0>
 LRT_DEV int ClosestHitDualGrid(const F3& o, const F3& db, bool hasS, const F3& ds, int li, const float4& lightSph,
                                const GridView& g, float& tOut, bool& lit, GridStats* st = nullptr) {
     GridQuery q;
-    GridDualInit(q, o, db, hasS, ds, li, lightSph, g, st);
-    while (q.busy) GridDualStep(q, g, st);
+    GridDualInit<kL>(q, o, db, hasS, ds, li, lightSph, g, st);
+    while (q.busy) GridDualStep<kL>(q, g, st);
     lit = q.lit;
     tOut = q.bestT;
     return q.best;

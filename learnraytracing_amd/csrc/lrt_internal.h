@@ -28,6 +28,7 @@
 #include <climits>
 #include <cmath>
 #include <mutex>
+#include <type_traits>
 #include <string>
 #include <vector>
 
@@ -95,6 +96,7 @@ struct KernelArgs {
     BvhView bv;
     GridView gv;
     int bvh_stack_offset;   // bytes into dynamic LDS
+    int grid_lds_offset;    // pool kernel, LRT_POOL_GRID_WPB blocks: the grid's LDS copy (bytes), or 0
     float4* ovf;            // recursion stack levels >= kTraceLdsLevels (null when maxDepth fits)
     unsigned long long* wtrace;   // LRT_EXP_WAVETRACE builds only: per-wave start/end/ids
     unsigned long long* tiles;    // this launch's counters: [q] tile queue, [kV0Queues + q] finished

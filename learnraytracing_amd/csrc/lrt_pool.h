@@ -59,7 +59,7 @@ __device__ __forceinline__ KArgPtr opaque_args() { return nullptr; }
 #ifndef LRT_GRID_BIG_LDS
 #define LRT_GRID_BIG_LDS 1
 #endif
-template <int kAcc>
+template <int kAcc, int kW>
 __device__ __forceinline__ GridView pool_grid_view(float4* smem) {
     GridView g = opaque_args()->gv;
     if (LRT_GRID_BIG_LDS) {
@@ -67,8 +67,30 @@ __device__ __forceinline__ GridView pool_grid_view(float4* smem) {
         g.bsph = b;
         g.bid = reinterpret_cast<const int*>(b + g.nbig);
     }
+    if (kW > 1) {   // the block's copy of the cells and their spheres (pool_grid_lds)
+        char* base = reinterpret_cast<char*>(smem) + opaque_args()->grid_lds_offset;
+        const unsigned ncell = (unsigned)(g.nx * g.ny * g.nz), nref = g.cells_refs;
+        g.rsph = reinterpret_cast<const float4*>(base);
+        g.cells = reinterpret_cast<const uint2*>(base + 16 * nref);
+        g.rid = reinterpret_cast<const int*>(base + 16 * nref + 8 * ncell);
+    }
     return g;
 }
+
+// Blocks of kW > 1 waves (LRT_POOL_GRID_WPB, grid instances): the waves of a block share one
+// LDS copy of the grid -- the cell ranges, the cell-ordered spheres and their indices
+// (config 4: 1,044 cells and 1,742 references, 43 KB) -- so the walk's dependent loads are LDS
+// reads (~50 cycles) instead of L1/L2 hits. Each wave keeps its own recursion stack, in kLv
+// levels of LDS (the rest in the global overflow stack) so that the 16 stacks and the grid
+// fit in the CU's 160 KB.
+#ifndef LRT_POOL_GRID_WPB
+#define LRT_POOL_GRID_WPB 16
+#endif
+#ifndef LRT_POOL_GRID_LDS_LEVELS
+#define LRT_POOL_GRID_LDS_LEVELS 7
+#endif
+template <int kW>
+constexpr int pool_lds_levels() { return kW > 1 ? LRT_POOL_GRID_LDS_LEVELS : kTraceLdsLevels; }
 
 #ifndef LRT_POOL_OVF_ZERO
 #define LRT_POOL_OVF_ZERO 1
@@ -77,27 +99,35 @@ __device__ __forceinline__ GridView pool_grid_view(float4* smem) {
 #ifndef LRT_POOL_GRID_WAVES
 #define LRT_POOL_GRID_WAVES LRT_V0_WAVES_PER_EU
 #endif
-template <int MAXD, bool kLds, int kAcc, int kPix, int kNS = 0>
-__global__ __launch_bounds__(64, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0_WAVES_PER_EU) void pool_kernel(
+template <int MAXD, bool kLds, int kAcc, int kPix, int kNS = 0, int kW = 1>
+__global__ __launch_bounds__(64 * kW, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0_WAVES_PER_EU) void pool_kernel(
     const KernelArgs a) {
     static_assert(kNS == 0 || (kLds && !kAcc), "a fixed sphere count is for the LDS linear scan");
+    static_assert(kW == 1 || (kAcc == kAccGrid && !kLds), "multi-wave blocks: the grid instance");
+    constexpr int kLv = pool_lds_levels<kW>();   // recursion stack levels in LDS
     // LDS as trace_kernel: [recursion stack kTraceLdsLevels x 64][powf tables][renormalize
     // table unless kAcc][spheres][materials][lights][bvh stack at a.bvh_stack_offset]
     extern __shared__ float4 smem[];
-    const int lane = threadIdx.x;
-    double* s_pow = reinterpret_cast<double*>(smem + kTraceLdsLevels * 64);
+    const int lane = kW > 1 ? (int)(threadIdx.x & 63u) : (int)threadIdx.x;
+    const int tid = threadIdx.x;   // fills of the block-shared LDS
+    // this wave's place among all waves (kW > 1: several per block, each as a block of one)
+    const int wave = kW > 1 ? (int)(threadIdx.x >> 6) : 0;
+    const int wid = (int)blockIdx.x * kW + wave;
+    const int nwaves = (int)gridDim.x * kW;
+    (void)nwaves;
+    double* s_pow = reinterpret_cast<double*>(smem + kW * kLv * 64);
     {
         const libm::PowTables g = libm::pow_tables();
-        for (int i = lane; i < 16; i += 64) {
+        for (int i = tid; i < 16; i += 64 * kW) {
             s_pow[i] = g.invc[i];
             s_pow[16 + i] = g.logc[i];
         }
-        for (int i = lane; i < 32; i += 64) reinterpret_cast<uint64_t*>(s_pow + 32)[i] = g.exp2[i];
+        for (int i = tid; i < 32; i += 64 * kW) reinterpret_cast<uint64_t*>(s_pow + 32)[i] = g.exp2[i];
     }
     constexpr int kLutBytes = kAcc ? 0 : kRenormBytes;
     float* s_lut = kAcc ? nullptr : reinterpret_cast<float*>(s_pow + 64);
     if (!kAcc) renorm_lut_fill(s_lut, lane, 64);
-    float4* s_sph = smem + kTraceLdsLevels * 64 + (kPowTableBytes + kLutBytes) / 16;
+    float4* s_sph = smem + kW * kLv * 64 + (kPowTableBytes + kLutBytes) / 16;
     float4* s_mat = s_sph + a.count;
     int* s_lights = reinterpret_cast<int*>(s_mat + 3 * a.count);
     if (kLds) {
@@ -107,10 +137,19 @@ __global__ __launch_bounds__(64, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0
     }
     if (kAcc == kAccGrid && LRT_GRID_BIG_LDS) {   // (pool_grid_view)
         float4* b = reinterpret_cast<float4*>(reinterpret_cast<char*>(smem) + a.bvh_stack_offset);
-        for (int i = lane; i < a.gv.nbig; i += 64) {
+        for (int i = tid; i < a.gv.nbig; i += 64 * kW) {
             b[i] = a.gv.bsph[i];
             reinterpret_cast<int*>(b + a.gv.nbig)[i] = a.gv.bid[i];
         }
+    }
+    if (kW > 1) {   // the grid's LDS copy (pool_grid_view)
+        char* base = reinterpret_cast<char*>(smem) + a.grid_lds_offset;
+        const int ncell = a.gv.nx * a.gv.ny * a.gv.nz, nref = (int)a.gv.cells_refs;
+        for (int i = tid; i < nref; i += 64 * kW) {
+            reinterpret_cast<float4*>(base)[i] = a.gv.rsph[i];
+            reinterpret_cast<int*>(base + 16 * nref + 8 * ncell)[i] = a.gv.rid[i];
+        }
+        for (int i = tid; i < ncell; i += 64 * kW) reinterpret_cast<uint2*>(base + 16 * nref)[i] = a.gv.cells[i];
     }
     __syncthreads();
     SceneView sc;
@@ -129,9 +168,9 @@ __global__ __launch_bounds__(64, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0
     sc.bstk = reinterpret_cast<unsigned short*>(reinterpret_cast<char*>(smem) + a.bvh_stack_offset) + lane;
     sc.bstride = 64;
 #ifdef LRT_EXP_SECSTATS
-    __shared__ unsigned long long s_sectime[2 + 3 * kSecN];
+    __shared__ unsigned long long s_sectime[kW][2 + 3 * kSecN];
     sc.secstats = a.wtrace;
-    sc.sectime = s_sectime;
+    sc.sectime = s_sectime[wave];
     if (lane == 0) {
         for (int k = 0; k < 2 + 3 * kSecN; ++k) sc.sectime[k] = 0;
         sc.sectime[0] = kSecOther;
@@ -141,32 +180,32 @@ __global__ __launch_bounds__(64, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0
 #ifdef LRT_EXP_WAVETRACE
     const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    float4* const lstk = smem + lane;   // this lane's recursion stack (LDS)
-    const size_t gtid = (size_t)blockIdx.x * 64 + lane;
-    const size_t gthreads = (size_t)gridDim.x * 64;
-    // Levels >= kTraceLdsLevels (MAXD > 8) in the global overflow stack: a u16 per level (the
+    float4* const lstk = smem + wave * kLv * 64 + lane;   // this lane's recursion stack (LDS)
+    const size_t gtid = (size_t)wid * 64 + lane;
+    const size_t gthreads = (size_t)nwaves * 64;
+    // Levels >= kLv (MAXD > 8, or kW > 1) in the global overflow stack: a u16 per level (the
     // material id, bit 15 set when the level's matE + lightE is exactly +0, which then needs no
     // float4 at all -- the fold adds the literal +0 the stored value was, parallel.cpp:214) and
     // the float4 only for the others. Deep levels are mostly glass and metal chains, whose
     // events add nothing (LRT_POOL_OVF_ZERO=0: a float4 per level, round 3).
     float4* const gstk = a.ovf + gtid;
     unsigned short* const gid =
-        reinterpret_cast<unsigned short*>(a.ovf + gthreads * (size_t)(a.maxDepth - kTraceLdsLevels)) + gtid;
+        reinterpret_cast<unsigned short*>(a.ovf + gthreads * (size_t)(a.maxDepth - kLv)) + gtid;
     auto put = [&](int lvl, float4 v) {
-        if (MAXD <= kTraceLdsLevels || lvl < kTraceLdsLevels) {
+        if (MAXD <= kLv || lvl < kLv) {
             lstk[lvl * 64] = v;
         } else if (LRT_POOL_OVF_ZERO) {
-            const size_t o = (size_t)(lvl - kTraceLdsLevels) * gthreads;
+            const size_t o = (size_t)(lvl - kLv) * gthreads;
             const bool z = (__float_as_uint(v.x) | __float_as_uint(v.y) | __float_as_uint(v.z)) == 0u;
             gid[o] = (unsigned short)(__float_as_int(v.w) | (z ? 0x8000 : 0));
             if (!z) gstk[o] = v;
         } else {
-            gstk[(size_t)(lvl - kTraceLdsLevels) * gthreads] = v;
+            gstk[(size_t)(lvl - kLv) * gthreads] = v;
         }
     };
     auto get = [&](int lvl) -> float4 {
-        if (MAXD <= kTraceLdsLevels || lvl < kTraceLdsLevels) return lstk[lvl * 64];
-        const size_t o = (size_t)(lvl - kTraceLdsLevels) * gthreads;
+        if (MAXD <= kLv || lvl < kLv) return lstk[lvl * 64];
+        const size_t o = (size_t)(lvl - kLv) * gthreads;
         if (LRT_POOL_OVF_ZERO) {
             const unsigned t = gid[o];
             if (t & 0x8000u) return make_float4(0.0f, 0.0f, 0.0f, __int_as_float((int)(t & 0x7fffu)));
@@ -174,7 +213,7 @@ __global__ __launch_bounds__(64, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0
         return gstk[o];
     };
     // this wave's colour slots: RGB, 12 B per sample (the 4th float was never read)
-    float* const slots = a.colbuf + (size_t)blockIdx.x * a.poolSlots * 3;
+    float* const slots = a.colbuf + (size_t)wid * a.poolSlots * 3;
 
     constexpr int TX = PoolTile<kPix>::X, TY = PoolTile<kPix>::Y;
     constexpr int kRoundFrames = kPoolSamples / kPix;
@@ -186,11 +225,12 @@ __global__ __launch_bounds__(64, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0
     const unsigned long long below = (1ull << lane) - 1ull;   // lanes before this one
     int rays = 0;
     // tile queues, as v0: block b serves queue b % kV0Queues (XCD-local counters)
+    // (kW > 1: the block's waves share its queue, so that a queue's counters stay in one XCD)
     const int q = blockIdx.x % kV0Queues;
-    const int bq = ((int)gridDim.x - q + kV0Queues - 1) / kV0Queues;
+    const int bq = (((int)gridDim.x - q + kV0Queues - 1) / kV0Queues) * kW;   // waves serving queue q
     const int nq = (ntiles - q + kV0Queues - 1) / kV0Queues;
     unsigned long long* ctr = a.tiles + q * kCtrStride;
-    for (int i = blockIdx.x / kV0Queues; i < nq;) {
+    for (int i = (int)(blockIdx.x / kV0Queues) * kW + wave; i < nq;) {
         const int task = q + kV0Queues * i;
         const int tile = a.perm ? a.perm[task] : task;   // heaviest-first order (tile_order)
         const unsigned long long tt0 = a.tcost ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -288,8 +328,8 @@ __global__ __launch_bounds__(64, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0
                     const bool hasS = pend && dl.on;
                     if constexpr (kAcc == kAccGrid) {
                         const float4 ls = hasS ? sc.sph[dl.li] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                        const GridView gv = pool_grid_view<kAcc>(smem);
-                        nid = ClosestHitDualGrid(r.orig, r.dir, hasS, dl.l, dl.li, ls, gv, nt, lit);
+                        const GridView gv = pool_grid_view<kAcc, kW>(smem);
+                        nid = ClosestHitDualGrid<(kW > 1 ? 1 : 0)>(r.orig, r.dir, hasS, dl.l, dl.li, ls, gv, nt, lit);
                     } else if constexpr (kAcc == kAccBvh) {
                         if (coherent) {
                             nid = ClosestHitBVH(r.orig, r.dir, sc.bv, nt, sc.bstk, sc.bstride, nullptr, true);
@@ -327,7 +367,7 @@ __global__ __launch_bounds__(64, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0
                         if (depth < a.maxDepth) {
                             F3 lightE;
                             dl.on = false;
-                            if constexpr (kAcc == kAccGrid) sc.gv = pool_grid_view<kAcc>(smem);   // other lights' shadow rays
+                            if constexpr (kAcc == kAccGrid) sc.gv = pool_grid_view<kAcc, kW>(smem);   // other lights' shadow rays
                             const F3 X = ScatterDir<kAcc, kNS>(mat, nid, r, rec, lightE, rays, rng, sc, &dl, coherent);
                             sec_count(sc, kSecPost);
                             const F3 dir = renormalize(normalize(X), sc.rnlut);   // Ray(rec.pos, normalize(X))
@@ -401,7 +441,7 @@ __global__ __launch_bounds__(64, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0
     sec_enter(sc, kSecOther, false);
     if (lane == 0)
         for (int k = 0; k < kSecN; ++k) {
-            unsigned long long* g = sc.secstats + 3 * (k + kSecN * (blockIdx.x & 15));
+            unsigned long long* g = sc.secstats + 3 * (k + kSecN * (wid & 15));
             atomicAdd(g, sc.sectime[2 + kSecN + k]);
             atomicAdd(g + 1, sc.sectime[2 + 2 * kSecN + k]);
             atomicAdd(g + 2, sc.sectime[2 + k]);
@@ -409,10 +449,10 @@ __global__ __launch_bounds__(64, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0
 #endif
 #ifdef LRT_EXP_WAVETRACE
     if (lane == 0) {
-        a.wtrace[4 * blockIdx.x + 0] = wt0;
-        a.wtrace[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
-        a.wtrace[4 * blockIdx.x + 2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
-        a.wtrace[4 * blockIdx.x + 3] = __builtin_amdgcn_s_getreg((15 << 11) | 20);   // XCC_ID
+        a.wtrace[4 * wid + 0] = wt0;
+        a.wtrace[4 * wid + 1] = __builtin_amdgcn_s_memrealtime();
+        a.wtrace[4 * wid + 2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+        a.wtrace[4 * wid + 3] = __builtin_amdgcn_s_getreg((15 << 11) | 20);   // XCC_ID
     }
 #endif
     const unsigned long long total = wave_sum((unsigned long long)rays);

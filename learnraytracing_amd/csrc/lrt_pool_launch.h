@@ -6,20 +6,47 @@
 
 namespace lrt {
 
+// Waves per block of the grid instance (LRT_POOL_GRID_WPB blocks share the grid's LDS copy);
+// 1 when the grid does not fit beside the waves' stacks, or with LRT_POOL_GRID_WPB=1 (A/B).
+inline int pool_grid_wpb(const KernelArgs& a, size_t stack_w, size_t shared_b, size_t* grid_b) {
+    const size_t ncell = (size_t)a.gv.nx * a.gv.ny * a.gv.nz, nref = a.gv.cells_refs;
+    *grid_b = (16 * nref + 8 * ncell + 4 * nref + 15) / 16 * 16;
+    static int env = -1;
+    if (env < 0) {
+        const char* v = getenv("LRT_POOL_GRID_WPB");
+        env = v ? atoi(v) : LRT_POOL_GRID_WPB;
+    }
+    if (env != LRT_POOL_GRID_WPB || !a.gv.on || a.gv.nx == 0) return 1;
+    int dev = 0, maxb = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&maxb, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess)
+        return 1;
+    return LRT_POOL_GRID_WPB * stack_w + shared_b + *grid_b <= (size_t)maxb ? LRT_POOL_GRID_WPB : 1;
+}
+
 template <int MAXD, int kPix>
 int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     constexpr int TX = PoolTile<kPix>::X, TY = PoolTile<kPix>::Y;
+    constexpr int kW = LRT_POOL_GRID_WPB;
     const long long ntiles = (long long)((xc + TX - 1) / TX) * ((rows + TY - 1) / TY);
     const int acc = a.gv.on ? kAccGrid : a.bv.on ? kAccBvh : kAccScan;
-    const size_t stack = sizeof(float4) * kTraceLdsLevels * 64 + kPowTableBytes + (acc ? 0 : kRenormBytes);
-    const size_t scene = lds ? sizeof(float4) * (4 * (size_t)a.count + (size_t)(a.nlights + 3) / 4 + 1) : 0;
-    a.bvh_stack_offset = (int)(stack + scene);
     // the BVH's traversal stack, or the grid's first-tested spheres (pool_grid_view)
     const size_t bstk = acc == kAccBvh ? sizeof(unsigned short) * ctx().bvh_stack_levels * 64
                         : acc == kAccGrid ? (sizeof(float4) + sizeof(int)) * (size_t)a.gv.nbig : 0;
-    const size_t ldsb = stack + scene + bstk;
+    size_t grid_b = 0;
+    const int wpb = acc == kAccGrid && !lds
+                        ? pool_grid_wpb(a, sizeof(float4) * pool_lds_levels<kW>() * 64,
+                                        kPowTableBytes + (bstk + 15) / 16 * 16, &grid_b)
+                        : 1;
+    const int lv = wpb > 1 ? pool_lds_levels<kW>() : kTraceLdsLevels;   // recursion stack levels in LDS
+    const size_t stack = sizeof(float4) * lv * 64 * wpb + kPowTableBytes + (acc ? 0 : kRenormBytes);
+    const size_t scene = lds ? sizeof(float4) * (4 * (size_t)a.count + (size_t)(a.nlights + 3) / 4 + 1) : 0;
+    a.bvh_stack_offset = (int)(stack + scene);
+    a.grid_lds_offset = wpb > 1 ? (int)(stack + (bstk + 15) / 16 * 16) : 0;
+    const size_t ldsb = wpb > 1 ? stack + (bstk + 15) / 16 * 16 + grid_b : stack + scene + bstk;
     const bool fixed = lds && acc == kAccScan && a.count == kFixedSpheres;
     const void* kern = acc == kAccGrid ? (lds ? (const void*)pool_kernel<MAXD, true, kAccGrid, kPix>
+                                          : wpb > 1 ? (const void*)pool_kernel<MAXD, false, kAccGrid, kPix, 0, kW>
                                               : (const void*)pool_kernel<MAXD, false, kAccGrid, kPix>)
                        : acc == kAccBvh ? (lds ? (const void*)pool_kernel<MAXD, true, kAccBvh, kPix>
                                                : (const void*)pool_kernel<MAXD, false, kAccBvh, kPix>)
@@ -27,13 +54,25 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
                           : lds ? (const void*)pool_kernel<MAXD, true, kAccScan, kPix>
                                 : (const void*)pool_kernel<MAXD, false, kAccScan, kPix>);
     int per_cu = 0;
-    hipError_t e = occupancy(&per_cu, kern, 64, ldsb);
+    if (wpb > 1) {   // dynamic LDS above the default limit (once per instance: the device's maximum)
+        static bool raised = false;
+        if (!raised) {
+            int dev = 0, maxb = 0;
+            if (hipGetDevice(&dev) == hipSuccess &&
+                hipDeviceGetAttribute(&maxb, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) == hipSuccess)
+                (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, maxb);
+            raised = true;
+        }
+    }
+    hipError_t e = occupancy(&per_cu, kern, 64 * wpb, ldsb);
     if (e != hipSuccess) return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
     if (per_cu < 1) return fail(LRT_E_INVALID, "pool_kernel does not fit on a CU");
     int cus = ctx().num_cus;
     for (const auto& m : ctx().masked_streams)
         if (m.first == s) cus = m.second;
-    long long blocks = std::max((long long)per_cu * cus, (long long)kV0Queues);   // a block per queue (as v0)
+    // a block per queue (as v0: queue q is served by blocks q, q + kV0Queues, ...), no more
+    // blocks than tiles (kW > 1: the block's waves beyond its queue's tiles find none)
+    long long blocks = std::max((long long)per_cu * cus, (long long)kV0Queues);
     if (blocks > ntiles) blocks = ntiles;
     const dim3 grid((unsigned)blocks);
     a.ovf = nullptr;
@@ -51,13 +90,14 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
         a.regenMin = env;
     }
     a.poolSlots = kPix * std::min(a.frames, kPoolSamples / kPix);   // one round's samples
-    e = hipMallocAsync((void**)&a.colbuf, sizeof(float) * 3 * (size_t)a.poolSlots * grid.x, s);
+    const size_t nwaves = (size_t)grid.x * wpb;
+    e = hipMallocAsync((void**)&a.colbuf, sizeof(float) * 3 * (size_t)a.poolSlots * nwaves, s);
     if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(pool colour slots)");
-    if (a.maxDepth > kTraceLdsLevels) {
-        const size_t gthreads = (size_t)grid.x * 64;
+    if (a.maxDepth > lv) {
+        const size_t gthreads = nwaves * 64;
         // float4 levels, then the u16 level tags (lrt_pool.h)
         e = hipMallocAsync((void**)&a.ovf, (sizeof(float4) + sizeof(unsigned short)) * gthreads *
-                                               (size_t)(a.maxDepth - kTraceLdsLevels), s);
+                                               (size_t)(a.maxDepth - lv), s);
         if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(trace stack overflow)");
     }
 #ifdef LRT_EXP_SECSTATS
@@ -65,7 +105,7 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     a.wtrace = d_sec;
 #endif
 #ifdef LRT_EXP_WAVETRACE
-    a.wtrace = wavetrace_buffer(grid.x);
+    a.wtrace = wavetrace_buffer((unsigned)nwaves);
 #endif
     bool record = false;
     Context::TileOrder* users[2];
@@ -88,6 +128,7 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     }
     if (acc == kAccGrid) {
         if (lds) pool_kernel<MAXD, true, kAccGrid, kPix><<<grid, 64, ldsb, s>>>(a);
+        else if (wpb > 1) pool_kernel<MAXD, false, kAccGrid, kPix, 0, kW><<<grid, 64 * kW, ldsb, s>>>(a);
         else pool_kernel<MAXD, false, kAccGrid, kPix><<<grid, 64, ldsb, s>>>(a);
     } else if (acc == kAccBvh) {
         if (lds) pool_kernel<MAXD, true, kAccBvh, kPix><<<grid, 64, ldsb, s>>>(a);
@@ -119,9 +160,9 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     // sorted order, 3 recording with the order borrowed from the same geometry, 4 recording in
     // the probe's order
     snprintf(g_last_launch, sizeof(g_last_launch),
-             "kernel=pool_kernel maxd=%d lds=%d bvh=%d acc=%s pix=%d ns=%d grid=%u tasks=%lld order=%d per_cu=%d", MAXD,
-             lds ? 1 : 0, acc == kAccBvh ? 1 : 0, acc_name(acc), kPix, fixed ? kFixedSpheres : 0, grid.x, ntiles,
-             !users[0] ? 0 : !record ? 2 : probed ? 4 : users[1] ? 3 : 1, per_cu);
+             "kernel=pool_kernel maxd=%d lds=%d bvh=%d acc=%s pix=%d ns=%d grid=%u tasks=%lld order=%d per_cu=%d wpb=%d",
+             MAXD, lds ? 1 : 0, acc == kAccBvh ? 1 : 0, acc_name(acc), kPix, fixed ? kFixedSpheres : 0, grid.x, ntiles,
+             !users[0] ? 0 : !record ? 2 : probed ? 4 : users[1] ? 3 : 1, per_cu, wpb);
 #ifdef LRT_EXP_SECSTATS
     secstats_dump(d_sec, s);
 #endif

@@ -389,6 +389,7 @@ int upload_scene(Context& c, const lrt_sphere* s, const lrt_material* m, int n) 
         g.errk = G.errk;
         g.ext = G.ext;
         g.on = 1;
+        g.cells_refs = (unsigned)G.rsph.size();
         c.grid_pick = accel ? grid_suitable(G) : grid_forced();
     }
     c.count = n;
