@@ -74,7 +74,7 @@ struct GridQuery {
     int best, li;
     int cx, cy, cz;   // current cell
     unsigned j, jend; // the current cell's sphere range still to test
-    int mode;         // 0 walking, 1 scanning every sphere (fallback), 2 this query is over
+    int mode;         // 0 walking, 2 this query is over
     bool sh, lit, busy;
 };
 
@@ -119,10 +119,16 @@ LRT_DEV void GridStart(GridQuery& q, const GridView& g, GridStats* st = nullptr)
     const float mo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(q.o.x), __builtin_fabsf(q.o.y)),
                                      __builtin_fabsf(q.o.z));
     if (!((mo + g.ext) * 1.52587890625e-05f < g.errk)) {
-        if (st) st->fallback += 1;
-        q.mode = 1;
-        q.j = 0;
-        q.jend = (unsigned)g.count;
+        // the fallback, here and not in the walk's loop (never in practice; keeping its
+        // pointer select and index select out of GridIter saves the walk ~20 scalar
+        // instructions and a vmcnt(0) wait per iteration): the reference's own scan over the
+        // whole scene in index order (the first-tested spheres again: an equal (cand, id)
+        // changes nothing, and the light's own test is no win over its bar)
+        if (st) {
+            st->fallback += 1;
+            st->spheres += g.count;
+        }
+        for (int k = 0; k < g.count; ++k) GridTest(q, g.all[k], k);
         return;
     }
     const float hix = GridPlane(g.lox, g.nx, g.hx), hiy = GridPlane(g.loy, g.ny, g.hy),
@@ -199,29 +205,23 @@ LRT_DEV void GridAdvance(GridQuery& q, const GridView& g, GridStats* st) {
     q.jend = cr.y;
     if (st) st->cells += 1;
 }
-// The fallback (mode 1, never in practice: origins ~8 scene sizes away) runs through the same
-// sphere test over the whole scene in index order (the reference's own scan, index = position):
-// one copy of the test in the loop.
+// (The fallback scan for far origins runs in GridStart, outside the loop.)
 template <int kL = 0>
 LRT_DEV void GridIter(GridQuery& q, const GridView& g, GridStats* st) {
     GridAdvance<kL>(q, g, st);
-    if (q.mode != 2 && q.j < q.jend) {
+    if (q.mode == 0 && q.j < q.jend) {
         if (st) st->spheres += 1;
         const unsigned j = q.j++;
-        const bool scan = q.mode == 1;
-        const float4 s = scan ? g.all[j] : LRT_GRID_LD(kL, g.rsph, j);
+        const float4 s = LRT_GRID_LD(kL, g.rsph, j);
         const float cand = GridCand(q.o, q.d, s);
         // the original index is read only when it can matter (a win or an exact tie)
         if (cand < q.bestT || (cand == q.bestT && q.best != -1)) {
-            const int id = scan ? (int)j : LRT_GRID_LD(kL, g.rid, j);
+            const int id = LRT_GRID_LD(kL, g.rid, j);
             if (GridBeats(q, cand, id)) {
                 q.bestT = cand;
                 q.best = id;
             }
         }
-        if (scan && q.j >= q.jend) q.mode = 2;
-    } else if (q.mode == 1) {
-        q.mode = 2;
     }
 }
 
