@@ -177,14 +177,9 @@ LRT_DEV void GridStart(GridQuery& q, const GridView& g, GridStats* st = nullptr)
 // lanes step along different axes issues one sequence, not three.
 template <int kL>
 LRT_DEV void GridAdvance(GridQuery& q, const GridView& g, GridStats* st) {
-    if (q.mode != 0 || q.j < q.jend) return;
+    if ((q.mode != 0) | (q.j < q.jend)) return;
     const float T = __builtin_fminf(__builtin_fminf(q.tnx, q.tny), q.tnz);
-    // nothing beyond this cell can win or tie (or T is NaN: nowhere to go)
-    if (q.bestT < T - (g.pad + 1e-5f * T) || !(T == T)) {
-        q.mode = 2;
-        return;
-    }
-    const bool ax = q.tnx == T, ay = !ax && q.tny == T, az = !ax && !ay;
+    const bool ax = q.tnx == T, ay = !ax & (q.tny == T), az = !ax & !ay;
     // each axis updates itself under its own condition (a select between an axis's new and old
     // value; selecting between fields instead turned into pointer selects, and the query into
     // scratch memory)
@@ -192,8 +187,11 @@ LRT_DEV void GridAdvance(GridQuery& q, const GridView& g, GridStats* st) {
     q.cx += ax ? 2 * ux - 1 : 0;
     q.cy += ay ? 2 * uy - 1 : 0;
     q.cz += az ? 2 * uz - 1 : 0;
-    if ((unsigned)q.cx >= (unsigned)g.nx || (unsigned)q.cy >= (unsigned)g.ny || (unsigned)q.cz >= (unsigned)g.nz) {
-        q.mode = 2;   // left the box
+    // the walk ends when nothing beyond this cell can win or tie (or T is NaN: nowhere to go),
+    // or when it leaves the box -- one exit, the conditions combined bitwise
+    if ((q.bestT < T - (g.pad + 1e-5f * T)) | !(T == T) | ((unsigned)q.cx >= (unsigned)g.nx) |
+        ((unsigned)q.cy >= (unsigned)g.ny) | ((unsigned)q.cz >= (unsigned)g.nz)) {
+        q.mode = 2;
         return;
     }
     // the stepped axis' next plane, the same expression GridStart uses
@@ -214,13 +212,15 @@ LRT_DEV void GridIter(GridQuery& q, const GridView& g, GridStats* st) {
         const unsigned j = q.j++;
         const float4 s = LRT_GRID_LD(kL, g.rsph, j);
         const float cand = GridCand(q.o, q.d, s);
-        // the original index is read only when it can matter (a win or an exact tie)
-        if (cand < q.bestT || (cand == q.bestT && q.best != -1)) {
+        // the original index is read only when it can matter (a win or an exact tie); then
+        // GridBeats reduces to (closer, or the lower index of a tie). Bitwise, not short-circuit:
+        // each && / || here was a divergent region of its own (exec bookkeeping per iteration).
+        const bool closer = cand < q.bestT;
+        if (closer | ((cand == q.bestT) & (q.best != -1))) {
             const int id = LRT_GRID_LD(kL, g.rid, j);
-            if (GridBeats(q, cand, id)) {
-                q.bestT = cand;
-                q.best = id;
-            }
+            const bool win = closer | (id < (q.best >= 0 ? q.best : q.li));
+            q.bestT = win ? cand : q.bestT;
+            q.best = win ? id : q.best;
         }
     }
 }
