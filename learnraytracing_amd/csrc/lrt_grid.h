@@ -82,7 +82,7 @@ LRT_DEV float GridPlane(float lo, int c, float h) { return lo + (float)c * h; }
 
 // (cand, index) order: does sphere `id` with candidate cand beat the query's best?
 LRT_DEV bool GridBeats(const GridQuery& q, float cand, int id) {
-    return cand < q.bestT || (cand == q.bestT && q.best != -1 && id < (q.best >= 0 ? q.best : q.li));
+    return (cand < q.bestT) | ((cand == q.bestT) & (q.best != -1) & (id < (q.best >= 0 ? q.best : q.li)));
 }
 LRT_DEV float GridCand(const F3& o, const F3& d, const float4& s) {   // maths.cpp:54-90
     const F3 rs = f3(s.x, s.y, s.z) - o;
@@ -109,7 +109,7 @@ LRT_DEV void GridStart(GridQuery& q, const GridView& g, GridStats* st = nullptr)
     // (a shadow query skips its own light: the light's candidate IS the bar, and a tie with the
     // same index changes nothing -- GridBeats is false for it)
     for (int k = 0; k < g.nbig; ++k)
-        if (q.best != -2 || g.bid[k] != q.li) GridTest(q, g.bsph[k], g.bid[k]);
+        if ((q.best != -2) | (g.bid[k] != q.li)) GridTest(q, g.bsph[k], g.bid[k]);
     q.inv = f3(rcp_rn(q.d.x), rcp_rn(q.d.y), rcp_rn(q.d.z));
     q.mode = 2;
     if (g.count == 0 || g.nx == 0) return;
@@ -137,7 +137,7 @@ LRT_DEV void GridStart(GridQuery& q, const GridView& g, GridStats* st = nullptr)
     float t0 = 0.0f, t1 = __builtin_inff();
     auto slab = [&](float o, float d, float inv, float lo, float hi) {
         if (d == 0.0f) {
-            if (o < lo || o > hi) t1 = -1.0f;
+            if ((o < lo) | (o > hi)) t1 = -1.0f;
             return;
         }
         const float a = (lo - o) * inv, b = (hi - o) * inv;
@@ -148,7 +148,7 @@ LRT_DEV void GridStart(GridQuery& q, const GridView& g, GridStats* st = nullptr)
     slab(q.o.y, q.d.y, q.inv.y, g.loy, hiy);
     slab(q.o.z, q.d.z, q.inv.z, g.loz, hiz);
     const float slack = g.pad + 1e-5f * t1;
-    if (t0 > t1 + slack || q.bestT < t0 - g.pad - 1e-5f * t0) return;   // misses the box, or beaten before it
+    if ((t0 > t1 + slack) | (q.bestT < t0 - g.pad - 1e-5f * t0)) return;   // misses the box, or beaten before it
     const F3 p = q.o + q.d * t0;
     auto cell = [](float p, float lo, float ih, int n) {
         const float f = (p - lo) * ih;
@@ -251,7 +251,7 @@ LRT_DEV bool ShadowReachesLightGrid(const F3& o, const F3& d, int li, const floa
     q.best = -2;
     q.li = li;
     GridStart(q, g, st);
-    while (q.mode != 2 && q.best == -2) GridIter(q, g, st);
+    while ((q.mode != 2) & (q.best == -2)) GridIter(q, g, st);
     return q.best == -2;
 }
 
@@ -275,7 +275,7 @@ LRT_DEV void GridDualInit(GridQuery& q, const F3& o, const F3& db, bool hasS, co
 template <int kL = 0>
 LRT_DEV void GridDualStep(GridQuery& q, const GridView& g, GridStats* st) {
     GridIter<kL>(q, g, st);
-    const bool qdone = q.mode == 2 || (q.sh && q.best != -2);
+    const bool qdone = (q.mode == 2) | (q.sh & (q.best != -2));
     if (qdone) {
         if (q.sh) {
             q.lit = q.best == -2;   // nothing beat the light

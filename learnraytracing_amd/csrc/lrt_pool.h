@@ -371,7 +371,7 @@ __global__ __launch_bounds__(64 * kW, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : L
                             const F3 X = ScatterDir<kAcc, kNS>(mat, nid, r, rec, lightE, rays, rng, sc, &dl, coherent);
                             sec_count(sc, kSecPost);
                             const F3 dir = renormalize(normalize(X), sc.rnlut);   // Ray(rec.pos, normalize(X))
-                            if (mat.type != 1 || dot(dir, rec.normal) > 0.0f) {    // Metal absorbs (:147)
+                            if ((mat.type != 1) | (dot(dir, rec.normal) > 0.0f)) {    // Metal absorbs (:147)
                                 if (a.ndl && prevLambert) matE = f3(0.0f, 0.0f, 0.0f);
                                 prevLambert = mat.type == 0;
                                 const F3 e = matE + lightE;

@@ -273,20 +273,17 @@ LRT_DEV void sec_count(const SceneView& sc, int sec) { sec_enter(sc, sec, true);
 // root if it lies in (tMin, closestT), else the second. (A branchless form -- sqrt for every
 // lane, selects -- measured slower: the divergent branch around the sqrt is cheap when no
 // lane takes it.)
+// Inside, the reference's if / else-if is taken as selects over both roots, its && as bitwise
+// ands: each short-circuit was a divergent region of its own, whose exec bookkeeping (scalar
+// instructions, a branch) cost more than the second root's add (the grid walk: profiles/r4_y).
 LRT_DEV void SphereRoots(float rsProj, float ifHit, float tMin, float& closestT, int& id, int i) {
     if (ifHit < 0.0f) {
         const float halfCut = sqrt_rn(-ifHit);
-        float t = rsProj - halfCut;
-        if (t > tMin && t < closestT) {
-            closestT = t;
-            id = i;
-        } else {
-            t = rsProj + halfCut;
-            if (t > tMin && t < closestT) {
-                closestT = t;
-                id = i;
-            }
-        }
+        const float t1 = rsProj - halfCut, t2 = rsProj + halfCut;
+        const bool ok1 = (t1 > tMin) & (t1 < closestT);
+        const bool ok2 = (t2 > tMin) & (t2 < closestT);
+        id = ok1 | ok2 ? i : id;
+        closestT = ok1 ? t1 : ok2 ? t2 : closestT;
     }
 }
 
