@@ -282,7 +282,7 @@ LRT_DEV void SphereRoots(float rsProj, float ifHit, float tMin, float& closestT,
         const float t1 = rsProj - halfCut, t2 = rsProj + halfCut;
         const bool ok1 = (t1 > tMin) & (t1 < closestT);
         const bool ok2 = (t2 > tMin) & (t2 < closestT);
-        id = ok1 | ok2 ? i : id;
+        id = (ok1 | ok2) ? i : id;
         closestT = ok1 ? t1 : ok2 ? t2 : closestT;
     }
 }
