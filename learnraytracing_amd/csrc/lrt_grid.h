@@ -94,12 +94,11 @@ LRT_DEV float GridCand(const F3& o, const F3& d, const float4& s) {   // maths.c
     const float t2 = rsProj + halfCut;
     return t1 > kMinT ? t1 : (t2 > kMinT ? t2 : __builtin_inff());
 }
-LRT_DEV void GridTest(GridQuery& q, const float4& s, int id) {
+LRT_DEV void GridTest(GridQuery& q, const float4& s, int id, bool on = true) {   // on: test at all
     const float cand = GridCand(q.o, q.d, s);
-    if (GridBeats(q, cand, id)) {
-        q.bestT = cand;
-        q.best = id;
-    }
+    const bool w = on & GridBeats(q, cand, id);   // selects, not a region
+    q.bestT = w ? cand : q.bestT;
+    q.best = w ? id : q.best;
 }
 
 // Starts q's walk along q.d (q.bestT / q.best / q.li set by the caller): the big spheres,
@@ -108,8 +107,7 @@ template <int kL = 0>
 LRT_DEV void GridStart(GridQuery& q, const GridView& g, GridStats* st = nullptr) {
     // (a shadow query skips its own light: the light's candidate IS the bar, and a tie with the
     // same index changes nothing -- GridBeats is false for it)
-    for (int k = 0; k < g.nbig; ++k)
-        if ((q.best != -2) | (g.bid[k] != q.li)) GridTest(q, g.bsph[k], g.bid[k]);
+    for (int k = 0; k < g.nbig; ++k) GridTest(q, g.bsph[k], g.bid[k], (q.best != -2) | (g.bid[k] != q.li));
     q.inv = f3(rcp_rn(q.d.x), rcp_rn(q.d.y), rcp_rn(q.d.z));
     q.mode = 2;
     if (g.count == 0 || g.nx == 0) return;
@@ -135,14 +133,11 @@ LRT_DEV void GridStart(GridQuery& q, const GridView& g, GridStats* st = nullptr)
                 hiz = GridPlane(g.loz, g.nz, g.hz);
     // the box's slab interval; an axis the ray does not move along constrains through o
     float t0 = 0.0f, t1 = __builtin_inff();
-    auto slab = [&](float o, float d, float inv, float lo, float hi) {
-        if (d == 0.0f) {
-            if ((o < lo) | (o > hi)) t1 = -1.0f;
-            return;
-        }
-        const float a = (lo - o) * inv, b = (hi - o) * inv;
-        t0 = __builtin_fmaxf(t0, __builtin_fminf(a, b));
-        t1 = __builtin_fminf(t1, __builtin_fmaxf(a, b));
+    auto slab = [&](float o, float d, float inv, float lo, float hi) {   // (selects: no region per axis)
+        const bool flat = d == 0.0f;
+        const float a = (lo - o) * inv, b = (hi - o) * inv;   // (inv = +-inf when flat: unused)
+        t0 = flat ? t0 : __builtin_fmaxf(t0, __builtin_fminf(a, b));
+        t1 = flat ? (((o < lo) | (o > hi)) ? -1.0f : t1) : __builtin_fminf(t1, __builtin_fmaxf(a, b));
     };
     slab(q.o.x, q.d.x, q.inv.x, g.lox, hix);
     slab(q.o.y, q.d.y, q.inv.y, g.loy, hiy);
