@@ -14,6 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # LRT_LIB overrides the library path (development A/B builds only)
 LIB_PATH = os.environ.get("LRT_LIB") or os.path.join(_HERE, "liblrt_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "lrt.h")
+DIAG_HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "lrt_diag.h")   # diagnostics
 
 LRT_OK = 0
 LRT_E_INVALID = -1
@@ -135,7 +136,7 @@ SIGNATURES = {
     "lrt_libm_eval_device": (_i, [_i, _vp, _vp, _c.c_longlong]),
     "lrt_bvh_stats": (_i, [_c.POINTER(Sphere), _i, _vp, _i, _vp]),
     "lrt_grid_stats": (_i, [_c.POINTER(Sphere), _i, _vp, _i, _vp]),
-    "lrt_bvh_eval": (_i, [_c.POINTER(Sphere), _i, _vp, _i, _vp, _vp, _i]),
+    "lrt_accel_eval": (_i, [_c.POINTER(Sphere), _i, _vp, _i, _i, _i, _vp, _vp]),
     "lrt_scatter_eval": (_i, [_c.POINTER(Sphere), _c.POINTER(Material), _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp,
                               _vp, _i]),
 }

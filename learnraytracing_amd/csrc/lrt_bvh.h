@@ -38,18 +38,28 @@ struct BvhView {
     int big0, nbig;         // spheres [big0, big0 + nbig) of lsph are tested before traversal:
                             // spheres far larger than the rest (the ground, r = 100) would make
                             // every ancestor box span the scene
+    // Exactness reach: each box is padded by the reference's hit excursion
+    // (hit_excursion, lrt_grid_build.h) for origins within sqrt(f2near) of every corner of the
+    // tree spheres' centre box (clo, chi); a ray from anywhere else inflates every box it tests
+    // by its own bound, hit_excursion(F + rmax, rmin) with F its farthest-corner distance
+    // (MakeSlabRay).
+    float clox, cloy, cloz, chix, chiy, chiz;
+    float f2near, rmax, rmin;
 };
 
-LRT_DEV void SlabTest(const float4& mn, const float4& mx, const F3& o, const F3& inv, float& tn, float& tf) {
+// ei: per-axis inflation of the box in t (e |inv_k|, a far ray's hit excursion e; 0 for the
+// others, which leaves every value as it was)
+LRT_DEV void SlabTest(const float4& mn, const float4& mx, const F3& o, const F3& inv, const F3& ei, float& tn,
+                      float& tf) {
     const float tx0 = (mn.x - o.x) * inv.x, tx1 = (mx.x - o.x) * inv.x;
     const float ty0 = (mn.y - o.y) * inv.y, ty1 = (mx.y - o.y) * inv.y;
     const float tz0 = (mn.z - o.z) * inv.z, tz1 = (mx.z - o.z) * inv.z;
-    // fminf/fmaxf drop a NaN operand (0 * inf on a slab plane): that axis then
-    // constrains nothing, which only ever keeps a node (conservative)
-    tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(tx0, tx1), __builtin_fminf(ty0, ty1)),
-                         __builtin_fminf(tz0, tz1));
-    tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(tx0, tx1), __builtin_fmaxf(ty0, ty1)),
-                         __builtin_fmaxf(tz0, tz1));
+    // fminf/fmaxf drop a NaN operand (0 * inf on a slab plane, inf - inf of an inflated
+    // infinite slab): that axis then constrains nothing, which only ever keeps a node
+    tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(tx0, tx1) - ei.x, __builtin_fminf(ty0, ty1) - ei.y),
+                         __builtin_fminf(tz0, tz1) - ei.z);
+    tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(tx0, tx1) + ei.x, __builtin_fmaxf(ty0, ty1) + ei.y),
+                         __builtin_fmaxf(tz0, tz1) + ei.z);
 }
 
 // The 4-wide traversals' slab test: t = fma(plane, inv, -o * inv), one FMA per plane
@@ -69,12 +79,24 @@ LRT_DEV void SlabTestFma(const float4& mn, const float4& mx, const F3& inv, cons
 // component of 0) makes plane * inv - o * inv an inf - inf = NaN, which the min/max would
 // resolve to the wrong extreme. Such rays keep the subtract-multiply form. With finite
 // products the extra margin is mo = 2^-22 * max_k |o_k * inv_k|, 4x the bound above.
+// Rays from beyond the BVH's near reach (f2near) take the subtract-multiply form with
+// every box inflated by their own hit excursion (oi then holds e |inv_k|; 0 for the other
+// rays of that form).
 struct SlabRay {
     F3 inv, oi;
     float mo;
     bool fma;
 };
-LRT_DEV SlabRay MakeSlabRay(const F3& o, const F3& d, float margin) {
+// hit_excursion (lrt_grid_build.h) for any sphere of the tree from an origin whose farthest
+// centre-box corner lies sqrt(f2) away, in float with a 2^-8 safety factor (its own rounding is
+// ~1e-7 relative); inf when it overflows or the origin is not finite.
+LRT_DEV float FarExcursion(float f2, const BvhView& bv) {
+    const float D = sqrt_rn(f2) * 1.00000095367431640625f + bv.rmax;
+    const float E = D * D * 1.9073486328125e-06f;   // 2^-19 D^2
+    const float e = (E / (sqrt_rn(bv.rmin * bv.rmin + E) + bv.rmin) + D * 1.430511474609375e-06f) * 1.00390625f;
+    return e < 3.0e38f ? e : __builtin_inff();
+}
+LRT_DEV SlabRay MakeSlabRay(const F3& o, const F3& d, const BvhView& bv) {
     SlabRay r;
     r.inv = f3(rcp_rn(d.x), rcp_rn(d.y), rcp_rn(d.z));   // = 1.0f / d (lrt_trace.h), shorter
     r.oi = f3(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
@@ -82,16 +104,26 @@ LRT_DEV SlabRay MakeSlabRay(const F3& o, const F3& d, float margin) {
                                      __builtin_fabsf(r.inv.z));
     const float mo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(o.x), __builtin_fabsf(o.y)), __builtin_fabsf(o.z));
     // margin = 1e-5 * extent + 1e-4 (build_bvh_host): every box coordinate is below 1e5 * margin
-    const float bound = mi * (1.0e5f * margin + mo);
-    r.fma = bound < 1.0e30f;   // false for inf / NaN too
+    const float bound = mi * (1.0e5f * bv.margin + mo);
+    const float fx = __builtin_fmaxf(__builtin_fabsf(o.x - bv.clox), __builtin_fabsf(o.x - bv.chix));
+    const float fy = __builtin_fmaxf(__builtin_fabsf(o.y - bv.cloy), __builtin_fabsf(o.y - bv.chiy));
+    const float fz = __builtin_fmaxf(__builtin_fabsf(o.z - bv.cloz), __builtin_fabsf(o.z - bv.chiz));
+    const float f2 = fx * fx + fy * fy + fz * fz;
+    const bool near = f2 <= bv.f2near;   // false for NaN too
+    r.fma = near & (bound < 1.0e30f);   // false for inf / NaN too
     r.mo = r.fma ? __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.oi.x), __builtin_fabsf(r.oi.y)),
                                    __builtin_fabsf(r.oi.z)) * 2.384185791015625e-07f
                  : 0.0f;
+    if (!r.fma) {
+        const float e = near ? 0.0f : FarExcursion(f2, bv);
+        r.oi = e > 0.0f ? f3(e * __builtin_fabsf(r.inv.x), e * __builtin_fabsf(r.inv.y), e * __builtin_fabsf(r.inv.z))
+                        : f3(0.0f, 0.0f, 0.0f);
+    }
     return r;
 }
 LRT_DEV void SlabTest4(const float4& mn, const float4& mx, const F3& o, const SlabRay& sr, float& tn, float& tf) {
     if (sr.fma) SlabTestFma(mn, mx, sr.inv, sr.oi, tn, tf);
-    else SlabTest(mn, mx, o, sr.inv, tn, tf);
+    else SlabTest(mn, mx, o, sr.inv, sr.oi, tn, tf);
 }
 
 // Host diagnostics (lrt_bvh_stats): node visits, sphere tests and the deepest traversal
@@ -111,7 +143,7 @@ static_assert(LRT_MAX_SPHERES <= 4096, "BVH4 stack entries hold 12-bit node indi
 template <int kForm>   // 1: FMA slab form, 2: subtract-multiply form (MakeSlabRay chooses per ray)
 LRT_DEV void SlabTestK(const float4& mn, const float4& mx, const F3& o, const SlabRay& sr, float& tn, float& tf) {
     if (kForm == 1) SlabTestFma(mn, mx, sr.inv, sr.oi, tn, tf);
-    else SlabTest(mn, mx, o, sr.inv, tn, tf);
+    else SlabTest(mn, mx, o, sr.inv, sr.oi, tn, tf);
 }
 
 // Pushes (node, mask) as stack entry sp (host builds track the depth reached).
@@ -203,7 +235,7 @@ LRT_DEV int ClosestHitBVH4Impl(const F3& o, const F3& d, const SlabRay& sr, cons
 
 LRT_DEV int ClosestHitBVH4(const F3& o, const F3& d, const BvhView& bv, float& tOut, unsigned short* stk, int stride,
                            BvhStats* st = nullptr) {
-    const SlabRay sr = MakeSlabRay(o, d, bv.margin);
+    const SlabRay sr = MakeSlabRay(o, d, bv);
     if (sr.fma) return ClosestHitBVH4Impl<1>(o, d, sr, bv, tOut, stk, stride, st);
     return ClosestHitBVH4Impl<2>(o, d, sr, bv, tOut, stk, stride, st);
 }
@@ -289,7 +321,7 @@ LRT_DEV bool ShadowReachesLightBVH4(const F3& o, const F3& d, int li, const floa
                                     unsigned short* stk, int stride, BvhStats* st = nullptr) {
     const float candL = SphereCand(o, d, lightSph);
     if (!(candL < kMaxT)) return false;   // the light is not hit at all (closestT starts at kMaxT)
-    const SlabRay sr = MakeSlabRay(o, d, bv.margin);
+    const SlabRay sr = MakeSlabRay(o, d, bv);
     if (sr.fma) return ShadowReachesLightBVH4Impl<1>(o, d, li, candL, sr, bv, stk, stride, st);
     return ShadowReachesLightBVH4Impl<2>(o, d, li, candL, sr, bv, stk, stride, st);
 }
@@ -354,7 +386,7 @@ LRT_DEV void TravTest(TravQuery& q, const BvhView& bv, int pos, const float4& s)
 LRT_DEV void TravStartBounce(TravQuery& q, const BvhView& bv) {
     q.sh = false;
     q.d = q.db;
-    q.sr = MakeSlabRay(q.o, q.d, bv.margin);
+    q.sr = MakeSlabRay(q.o, q.d, bv);
     q.bestT = kMaxT;
     q.best = -1;
     for (int j = 0; j < bv.nbig; ++j) TravTest(q, bv, bv.big0 + j, bv.lsph[bv.big0 + j]);
@@ -377,7 +409,7 @@ LRT_DEV void TravInit(TravQuery& q, const F3& o, const F3& db, bool hasS, const 
     }
     q.sh = true;
     q.d = ds;
-    q.sr = MakeSlabRay(o, ds, bv.margin);
+    q.sr = MakeSlabRay(o, ds, bv);
     q.bestT = candL;
     q.best = -2;
     for (int j = 0; j < bv.nbig; ++j) TravTest(q, bv, bv.big0 + j, bv.lsph[bv.big0 + j]);
@@ -650,7 +682,7 @@ LRT_DEV int ClosestHitBVH(const F3& o, const F3& d, const BvhView& bv, float& tO
                           BvhStats* st = nullptr, bool coherent = false) {
 #if LRT_PACKET_AVAILABLE
     if (coherent) {
-        const SlabRay sr = MakeSlabRay(o, d, bv.margin);
+        const SlabRay sr = MakeSlabRay(o, d, bv);
         if (__ballot(!sr.fma) == 0) return ClosestHitPacket(o, d, sr, bv, tOut, stk, stride);
     }
 #endif
@@ -662,7 +694,7 @@ LRT_DEV bool ShadowReachesLightBVH(const F3& o, const F3& d, int li, const float
 #if LRT_PACKET_AVAILABLE
     if (coherent) {
         const float candL = SphereCand(o, d, lightSph);
-        const SlabRay sr = MakeSlabRay(o, d, bv.margin);
+        const SlabRay sr = MakeSlabRay(o, d, bv);
         if (__ballot(!sr.fma) == 0) return candL < kMaxT && ShadowPacket(o, d, li, candL, sr, bv, stk, stride);
     }
 #endif

@@ -70,16 +70,18 @@ __global__ __launch_bounds__(64) void scatter_probe_kernel(SceneView sc, const i
     if (i < n) scatter_case<kAcc>(sc, i, ids, rays, recs, seeds, out, ret, counted, state, coherent != 0);
 }
 
-// lrt_bvh_eval's device side: one thread per ray, per-lane or packet traversal.
-__global__ __launch_bounds__(64) void bvh_probe_kernel(BvhView bv, const float* rays, int n, int* ids, float* ts,
-                                                       int packet) {
+// lrt_accel_eval's device side: one thread per ray; the BVH per lane or as a packet, or the grid.
+template <int kAcc>
+__global__ __launch_bounds__(64) void accel_probe_kernel(BvhView bv, GridView g, const float* rays, int n, int* ids,
+                                                         float* ts, int packet) {
     __shared__ unsigned short stk[kBvhStackLevels * 64];
     const int i = blockIdx.x * 64 + threadIdx.x;
     if (i >= n) return;
     const Ray r = make_ray(f3(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]),
                            f3(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]));
     float t = 0.0f;
-    ids[i] = ClosestHitBVH(r.orig, r.dir, bv, t, stk + threadIdx.x, 64, nullptr, packet != 0);
+    if constexpr (kAcc == kAccBvh) ids[i] = ClosestHitBVH(r.orig, r.dir, bv, t, stk + threadIdx.x, 64, nullptr, packet != 0);
+    else ids[i] = ClosestHitGrid(r.orig, r.dir, g, t);
     ts[i] = t;
 }
 
@@ -103,14 +105,7 @@ int lrt_bvh_stats(const lrt_sphere* spheres, int count, const float* rays, int n
     BvhHost H;
     build_bvh_host(spheres, count, sph, H);
     BvhView bv;
-    bv.nodes = H.nodes.data();
-    bv.lsph = H.lsph.data();
-    bv.lid = H.lid.data();
-    bv.margin = H.margin;
-    bv.on = 1;
-    bv.nnodes = (int)(H.nodes.size() / 8);
-    bv.big0 = H.big0;
-    bv.nbig = H.nbig;
+    bvh_view_host(H, bv);
     double sn = 0, ss = 0, mn = 0, ms = 0, bad = 0, msp = 0;
     unsigned short stk[kBvhStackLevels];
     for (int i = 0; i < n; ++i) {
@@ -235,11 +230,9 @@ int lrt_scatter_eval(const lrt_sphere* spheres, const lrt_material* materials, i
     if (lights.empty()) lights.push_back(0);   // never read (nlights = 0): keeps the copy non-empty
     sc.pow = libm::pow_tables();   // host addresses: the probe kernel sets its own
     sc.rnlut = nullptr;
-    sc.bv.margin = B.margin;
+    bvh_view_host(B, sc.bv);
     sc.bv.on = bvh ? 1 : 0;
     sc.bv.nnodes = bvh ? (int)(B.nodes.size() / 8) : 0;
-    sc.bv.big0 = B.big0;
-    sc.bv.nbig = B.nbig;
     if (!on_device) {
         sc.sph = sph.data();
         sc.mats = mats.data();
@@ -311,61 +304,84 @@ int lrt_scatter_eval(const lrt_sphere* spheres, const lrt_material* materials, i
     return LRT_OK;
 }
 
-int lrt_bvh_eval(const lrt_sphere* spheres, int count, const float* rays, int n, int* ids, float* ts, int mode) {
-    if (!spheres || count < 2 || !rays || !ids || !ts || n < 0 || mode < 0 || mode > 2)
-        return fail(LRT_E_INVALID, "bvh eval: invalid arguments");
+int lrt_accel_eval(const lrt_sphere* spheres, int count, const float* rays, int n, int accel, int mode, int* ids,
+                   float* ts) {
+    if (!spheres || count < 1 || !rays || !ids || !ts || n < 0 || accel < 1 || accel > 2 || mode < 0 || mode > 2 ||
+        (accel == 2 && mode == 2))
+        return fail(LRT_E_INVALID, "accel eval: invalid arguments");
+    if (accel == 1 && count < 2) return fail(LRT_E_INVALID, "accel eval: the BVH needs 2 spheres");
     std::vector<float4> sph(count);
     for (int i = 0; i < count; ++i) {
         const float r = spheres[i].radius;
         sph[i] = make_float4(spheres[i].center.x, spheres[i].center.y, spheres[i].center.z, r * r);
     }
     BvhHost H;
-    build_bvh_host(spheres, count, sph, H);
-    BvhView bv;
-    bv.margin = H.margin;
-    bv.on = 1;
-    bv.nnodes = (int)(H.nodes.size() / 8);
-    bv.big0 = H.big0;
-    bv.nbig = H.nbig;
+    GridHost G;
+    BvhView bv{};
+    if (accel == 1) {
+        build_bvh_host(spheres, count, sph, H);
+        bvh_view_host(H, bv);
+    } else {
+        build_grid_host(spheres, count, sph, G);
+    }
     if (mode == 0) {
-        bv.nodes = H.nodes.data();
-        bv.lsph = H.lsph.data();
-        bv.lid = H.lid.data();
+        const GridView g = accel == 2 ? grid_view_host(G, sph.data()) : GridView{};
         unsigned short stk[kBvhStackLevels];
         for (int i = 0; i < n; ++i) {
             const Ray r = make_ray(f3(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]),
                                    f3(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]));
-            ids[i] = ClosestHitBVH(r.orig, r.dir, bv, ts[i], stk, 1);
+            ids[i] = accel == 1 ? ClosestHitBVH(r.orig, r.dir, bv, ts[i], stk, 1) : ClosestHitGrid(r.orig, r.dir, g, ts[i]);
         }
         return LRT_OK;
     }
     if (n == 0) return LRT_OK;
-    void *d_nodes = nullptr, *d_lsph = nullptr, *d_lid = nullptr, *d_rays = nullptr, *d_ids = nullptr, *d_ts = nullptr;
-    hipError_t e = hipMalloc(&d_nodes, sizeof(float4) * std::max<size_t>(H.nodes.size(), 8));
-    if (e == hipSuccess) e = hipMalloc(&d_lsph, sizeof(float4) * H.lsph.size());
-    if (e == hipSuccess) e = hipMalloc(&d_lid, sizeof(int) * H.lid.size());
-    if (e == hipSuccess) e = hipMalloc(&d_rays, sizeof(float) * 6 * (size_t)n);
-    if (e == hipSuccess) e = hipMalloc(&d_ids, sizeof(int) * (size_t)n);
-    if (e == hipSuccess) e = hipMalloc(&d_ts, sizeof(float) * (size_t)n);
-    if (e == hipSuccess && !H.nodes.empty())
-        e = hipMemcpy(d_nodes, H.nodes.data(), sizeof(float4) * H.nodes.size(), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(d_lsph, H.lsph.data(), sizeof(float4) * H.lsph.size(), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(d_lid, H.lid.data(), sizeof(int) * H.lid.size(), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(d_rays, rays, sizeof(float) * 6 * (size_t)n, hipMemcpyHostToDevice);
-    if (e == hipSuccess) {
-        bv.nodes = (const float4*)d_nodes;
-        bv.lsph = (const float4*)d_lsph;
-        bv.lid = (const int*)d_lid;
-        bvh_probe_kernel<<<(unsigned)((n + 63) / 64), 64>>>(bv, (const float*)d_rays, n, (int*)d_ids, (float*)d_ts,
-                                                          mode == 2);
-        e = hipGetLastError();
+    std::vector<void*> owned;
+    auto up = [&](const void* src, size_t bytes) -> void* {   // a device copy (>= 16 B), owned
+        void* d = nullptr;
+        if (hipMalloc(&d, std::max<size_t>(bytes, 16)) != hipSuccess) return nullptr;
+        owned.push_back(d);
+        if (bytes && hipMemcpy(d, src, bytes, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+        return d;
+    };
+    std::vector<void*> need;
+    void* d_rays = up(rays, sizeof(float) * 6 * (size_t)n);
+    int* o_ids = nullptr;
+    float* o_ts = nullptr;
+    if (hipMalloc(&o_ids, sizeof(int) * (size_t)n) == hipSuccess) owned.push_back(o_ids);
+    if (hipMalloc(&o_ts, sizeof(float) * (size_t)n) == hipSuccess) owned.push_back(o_ts);
+    need = {d_rays, o_ids, o_ts};
+    GridView g{};
+    if (accel == 1) {
+        bv.nodes = (const float4*)up(H.nodes.data(), sizeof(float4) * H.nodes.size());
+        bv.lsph = (const float4*)up(H.lsph.data(), sizeof(float4) * H.lsph.size());
+        bv.lid = (const int*)up(H.lid.data(), sizeof(int) * H.lid.size());
+        need.insert(need.end(), {(void*)bv.nodes, (void*)bv.lsph, (void*)bv.lid});
+    } else {
+        g = grid_view_host(G, sph.data());
+        g.cells = (const uint2*)up(G.ranges.data(), sizeof(uint2) * G.ranges.size());
+        g.rsph = (const float4*)up(G.rsph.data(), sizeof(float4) * G.rsph.size());
+        g.rid = (const int*)up(G.rid.data(), sizeof(int) * G.rid.size());
+        g.bsph = (const float4*)up(G.bsph.data(), sizeof(float4) * G.bsph.size());
+        g.bid = (const int*)up(G.bid.data(), sizeof(int) * G.bid.size());
+        g.all = (const float4*)up(sph.data(), sizeof(float4) * sph.size());
+        need.insert(need.end(), {(void*)g.cells, (void*)g.rsph, (void*)g.rid, (void*)g.bsph, (void*)g.bid, (void*)g.all});
     }
+    auto release = [&]() {
+        for (void* p : owned) (void)hipFree(p);
+    };
+    if (std::find(need.begin(), need.end(), nullptr) != need.end()) {
+        release();
+        return fail(LRT_E_NOMEM, "accel eval: device allocation failed");
+    }
+    const unsigned blocks = (unsigned)((n + 63) / 64);
+    if (accel == 1) accel_probe_kernel<kAccBvh><<<blocks, 64>>>(bv, g, (const float*)d_rays, n, o_ids, o_ts, mode == 2);
+    else accel_probe_kernel<kAccGrid><<<blocks, 64>>>(bv, g, (const float*)d_rays, n, o_ids, o_ts, 0);
+    hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipDeviceSynchronize();
-    if (e == hipSuccess) e = hipMemcpy(ids, d_ids, sizeof(int) * (size_t)n, hipMemcpyDeviceToHost);
-    if (e == hipSuccess) e = hipMemcpy(ts, d_ts, sizeof(float) * (size_t)n, hipMemcpyDeviceToHost);
-    for (void* p : {d_nodes, d_lsph, d_lid, d_rays, d_ids, d_ts})
-        if (p) (void)hipFree(p);
-    if (e != hipSuccess) return fail(LRT_E_HIP, std::string("bvh eval: ") + hipGetErrorString(e));
+    if (e == hipSuccess) e = hipMemcpy(ids, o_ids, sizeof(int) * (size_t)n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(ts, o_ts, sizeof(float) * (size_t)n, hipMemcpyDeviceToHost);
+    release();
+    if (e != hipSuccess) return fail(LRT_E_HIP, std::string("accel eval: ") + hipGetErrorString(e));
     return LRT_OK;
 }
 

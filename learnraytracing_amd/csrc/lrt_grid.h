@@ -40,7 +40,15 @@ struct GridView {
     float hx, hy, hz;        // cell size per axis
     float ihx, ihy, ihz;     // 1 / cell size
     float pad;               // insertion padding (absolute)
-    float errk;              // a ray may walk if 2^-16 (max|o| + ext) < errk (= pad / 2)
+    // exactness reach (lrt_grid_build.h): an origin within sqrt(f2near) of every
+    // corner of the walked spheres' centre box (clo, chi): the walk alone is exact; otherwise,
+    // with dot(o, o) <= o2dda, the walk is exact up to tsafe from o, and a ray whose candidates
+    // could lie farther (GridFarT) scans every sphere at the end unless its answer came first;
+    // beyond (or NaN): the scan
+    float clox, cloy, cloz, chix, chiy, chiz;
+    float f2near, o2dda;
+    float tsafe;             // the walk finds every candidate up to tsafe from such an origin
+    float conea, coneb;      // a reference hit point at t lies within conea + coneb t of the box
     float ext;               // max |coordinate| of the box
     int on;
     unsigned cells_refs;     // entries of rsph / rid (the LDS copy's size, LRT_POOL_GRID_WPB)
@@ -74,6 +82,7 @@ struct GridQuery {
     int best, li;
     int cx, cy, cz;   // current cell
     unsigned j, jend; // the current cell's sphere range still to test
+    float farT;       // the scan is needed at the end unless bestT < farT (+inf: never)
     int mode;         // 0 walking, 2 this query is over
     bool sh, lit, busy;
 };
@@ -101,6 +110,45 @@ LRT_DEV void GridTest(GridQuery& q, const float4& s, int id, bool on = true) {  
     q.best = w ? id : q.best;
 }
 
+// For a ray from beyond the grid's near reach (o2near < |o|^2 <= o2dda) the walk finds every
+// candidate up to tsafe (the padding is sized for them, lrt_grid_build.h). A candidate beyond
+// lies within conea + coneb t of the grid's box (hit_excursion <= c1 D, D <= 1.004 t + 3.02 r),
+// a cone around the box: the t interval in which the ray is inside it is an intersection of 6
+// half-lines. Returns the t from which the walk's answer is not certain (less a margin), or
+// +inf when the cone beyond tsafe is empty. Conservative throughout; few rays come here.
+LRT_DEV float rcp_approx(float x) {   // within 1 ulp of 1 / x (v_rcp_f32); exact on the host
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcpf(x);
+#else
+    return 1.0f / x;
+#endif
+}
+LRT_DEV float sqrt_approx(float x) {   // within 1 ulp (v_sqrt_f32)
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_sqrtf(x);
+#else
+    return __builtin_sqrtf(x);
+#endif
+}
+LRT_DEV float GridFarT(const GridQuery& q, const GridView& g, float o2) {
+    const float a = g.conea + (sqrt_approx(o2) * 1.0000019073486328125f + g.ext) * 1.52587890625e-05f, b = g.coneb;
+    float tA = 0.0f, tB = __builtin_inff();
+    auto axis = [&](float o, float d, float lo, float hi) {
+        // lo - a - b t <= o + t d <= hi + a + b t:  (d + b) t >= lo - a - o,  (d - b) t <= hi + a - o
+        const float dp = d + b, dm = d - b, r1 = lo - a - o, r2 = hi + a - o;
+        const float q1 = r1 * rcp_approx(dp), q2 = r2 * rcp_approx(dm);   // (1 ulp: inside the slack)
+        tA = dp > 0.0f ? __builtin_fmaxf(tA, q1) : tA;
+        tB = dp < 0.0f ? __builtin_fminf(tB, q1) : ((dp == 0.0f) & (r1 > 0.0f)) ? -1.0f : tB;
+        tB = dm > 0.0f ? __builtin_fminf(tB, q2) : ((dm == 0.0f) & (r2 < 0.0f)) ? -1.0f : tB;
+        tA = dm < 0.0f ? __builtin_fmaxf(tA, q2) : tA;
+    };
+    axis(q.o.x, q.d.x, g.lox, GridPlane(g.lox, g.nx, g.hx));
+    axis(q.o.y, q.d.y, g.loy, GridPlane(g.loy, g.ny, g.hy));
+    axis(q.o.z, q.d.z, g.loz, GridPlane(g.loz, g.nz, g.hz));
+    const float lo = __builtin_fmaxf(tA, g.tsafe);
+    return lo < tB * 1.0000152587890625f + g.pad ? lo * 0.9999847412109375f - g.pad : __builtin_inff();
+}
+
 // Starts q's walk along q.d (q.bestT / q.best / q.li set by the caller): the big spheres,
 // then the cell where the ray enters the box.
 template <int kL = 0>
@@ -110,24 +158,24 @@ LRT_DEV void GridStart(GridQuery& q, const GridView& g, GridStats* st = nullptr)
     for (int k = 0; k < g.nbig; ++k) GridTest(q, g.bsph[k], g.bid[k], (q.best != -2) | (g.bid[k] != q.li));
     q.inv = f3(rcp_rn(q.d.x), rcp_rn(q.d.y), rcp_rn(q.d.z));
     q.mode = 2;
+    q.farT = __builtin_inff();
     if (g.count == 0 || g.nx == 0) return;
-    // The walk's rounding bound, 2^-18 (max|o| + tEnter + ext) <= 2^-16 (max|o| + ext) (tEnter is
-    // at most sqrt(3) (max|o| + ext)), must stay below errk; else (a huge origin, NaN) scan every
-    // sphere. Decided before the box test: that test's own rounding grows with |o| too.
-    const float mo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(q.o.x), __builtin_fabsf(q.o.y)),
-                                     __builtin_fabsf(q.o.z));
-    if (!((mo + g.ext) * 1.52587890625e-05f < g.errk)) {
-        // the fallback, here and not in the walk's loop (never in practice; keeping its
-        // pointer select and index select out of GridIter saves the walk ~20 scalar
-        // instructions and a vmcnt(0) wait per iteration): the reference's own scan over the
-        // whole scene in index order (the first-tested spheres again: an equal (cand, id)
-        // changes nothing, and the light's own test is no win over its bar)
-        if (st) {
-            st->fallback += 1;
-            st->spheres += g.count;
+    // Exactness needs the DDA's rounding (2^-18 (max|o| + tEnter + ext) <= 2^-16 (max|o| + ext);
+    // tEnter is at most sqrt(3) (max|o| + ext)) plus how far off its sphere the reference's own
+    // hit point can be (hit_excursion, growing with |c - o|) to stay inside the padding: true for
+    // every candidate when |o| is within the near reach (o2near), for those up to a distance
+    // when it is within o2dda (GridFarT), for none beyond: a huge origin, NaN or inf scans every
+    // sphere (GridFinish, farT = -inf). Decided before the box test: its rounding grows with |o|.
+    const float fx = __builtin_fmaxf(__builtin_fabsf(q.o.x - g.clox), __builtin_fabsf(q.o.x - g.chix));
+    const float fy = __builtin_fmaxf(__builtin_fabsf(q.o.y - g.cloy), __builtin_fabsf(q.o.y - g.chiy));
+    const float fz = __builtin_fmaxf(__builtin_fabsf(q.o.z - g.cloz), __builtin_fabsf(q.o.z - g.chiz));
+    if (!(fx * fx + fy * fy + fz * fz <= g.f2near)) {   // (rare: origins away from the spheres)
+        const float o2 = dot(q.o, q.o);
+        if (!(o2 <= g.o2dda)) {
+            q.farT = -__builtin_inff();
+            return;
         }
-        for (int k = 0; k < g.count; ++k) GridTest(q, g.all[k], k);
-        return;
+        q.farT = GridFarT(q, g, o2);
     }
     const float hix = GridPlane(g.lox, g.nx, g.hx), hiy = GridPlane(g.loy, g.ny, g.hy),
                 hiz = GridPlane(g.loz, g.nz, g.hz);
@@ -220,6 +268,21 @@ LRT_DEV void GridIter(GridQuery& q, const GridView& g, GridStats* st) {
     }
 }
 
+// The end of q's query: the scan of every sphere when the walk's answer is not certain
+// (GridFarT, or a huge origin): the reference's own scan over the whole scene in index order
+// (the spheres tested already again: an equal (cand, id) changes nothing, and a shadow query's
+// light is no win over its own bar). Out of the walk's loop (the walk keeps its pointer and
+// index selects out: ~20 scalar instructions and a vmcnt(0) wait per iteration, r4_x).
+LRT_DEV void GridFinish(GridQuery& q, const GridView& g, GridStats* st) {
+    if (!(q.bestT < q.farT)) {
+        if (st) {
+            st->fallback += 1;
+            st->spheres += g.count;
+        }
+        for (int k = 0; k < g.count; ++k) GridTest(q, g.all[k], k);
+    }
+}
+
 LRT_DEV int ClosestHitGrid(const F3& o, const F3& d, const GridView& g, float& tOut, GridStats* st = nullptr) {
     GridQuery q;
     q.o = o;
@@ -229,6 +292,7 @@ LRT_DEV int ClosestHitGrid(const F3& o, const F3& d, const GridView& g, float& t
     q.li = -1;
     GridStart(q, g, st);
     while (q.mode != 2) GridIter(q, g, st);
+    GridFinish(q, g, st);
     tOut = q.bestT;
     return q.best;
 }
@@ -247,6 +311,7 @@ LRT_DEV bool ShadowReachesLightGrid(const F3& o, const F3& d, int li, const floa
     q.li = li;
     GridStart(q, g, st);
     while ((q.mode != 2) & (q.best == -2)) GridIter(q, g, st);
+    if (q.best == -2) GridFinish(q, g, st);   // (a sphere that beat the light is an answer already)
     return q.best == -2;
 }
 
@@ -272,6 +337,7 @@ LRT_DEV void GridDualStep(GridQuery& q, const GridView& g, GridStats* st) {
     GridIter<kL>(q, g, st);
     const bool qdone = (q.mode == 2) | (q.sh & (q.best != -2));
     if (qdone) {
+        if (!q.sh | (q.best == -2)) GridFinish(q, g, st);
         if (q.sh) {
             q.lit = q.best == -2;   // nothing beat the light
             q.sh = false;

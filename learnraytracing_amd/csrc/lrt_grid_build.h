@@ -16,6 +16,53 @@
 
 namespace lrt {
 
+// ---- How far from its sphere the reference's hit point can lie ------------
+// HitSphere (maths.cpp:54-59) forms ifHit = dot(rs,rs) - rsProj^2 - r^2 (rs = c - o) by
+// cancellation. For a near-tangent ray its rounding, ~ulp(|rs|^2), can turn a miss into a
+// "hit", or move a hit, off the sphere: with D >= |c - o| + r, the point X = o + cand * d of
+// the candidate the reference computes satisfies |X - c| <= r + hit_excursion(D, r). (Forward
+// error analysis over the seven roundings of ifHit, rsProj and the roots and |d|^2 = 1 +- 12
+// eps of a normalised direction: |X - c|^2 <= (sqrt(r^2 + E) + f)^2 with E <= 30 eps D^2,
+// f <= 16 eps D; a brute-force search over near-tangent rays reaches 0.55 of it.) Small r:
+// ~1.4e-3 D; large r: ~E / 2r. The grid's padding and the BVH's boxes must cover it for every
+// ray they serve (the r4 verdict's mismatches: origins 40-400 units away).
+inline double hit_excursion(double D, double r) {
+    const double E = std::ldexp(D * D, -19);   // 32 eps D^2
+    return E / (std::sqrt(r * r + E) + r) + std::ldexp(24.0 * D, -24);
+}
+// Over the spheres `ids` of s: rs = max |c| + max r (so |c - o| + r <= |o| + rs for each),
+// rmin = min r.
+inline void sphere_reach(const lrt_sphere* s, const std::vector<int>& ids, double& rs, double& rmin) {
+    double cmax = 0.0, rmax = 0.0;
+    rmin = INFINITY;
+    for (int i : ids) {
+        const double x = s[i].center.x, y = s[i].center.y, z = s[i].center.z, r = std::fabs((double)s[i].radius);
+        cmax = std::max(cmax, std::sqrt(x * x + y * y + z * z));
+        rmax = std::max(rmax, r);
+        rmin = std::min(rmin, r);
+    }
+    rs = cmax + rmax;
+    if (!(rmin < INFINITY)) rmin = 0.0;
+}
+// The box of the centres of the spheres `ids` of s (the near test: an origin within a distance
+// of every corner of it is within that distance of every centre).
+inline void centre_box(const lrt_sphere* s, const std::vector<int>& ids, float clo[3], float chi[3]) {
+    for (int k = 0; k < 3; ++k) {
+        clo[k] = INFINITY;
+        chi[k] = -INFINITY;
+    }
+    for (int i : ids) {
+        const float c[3] = {s[i].center.x, s[i].center.y, s[i].center.z};
+        for (int k = 0; k < 3; ++k) {
+            clo[k] = std::min(clo[k], c[k]);
+            chi[k] = std::max(chi[k], c[k]);
+        }
+    }
+}
+// A squared-distance bound as a float that a ray's computed sum of three squares (relative
+// error <= 3 eps) can be compared with: at or below it, the distance is <= reach.
+inline float reach_sq(double reach) { return (float)(reach * reach * (1.0 - std::ldexp(1.0, -20))); }
+
 struct GridHost {
     std::vector<unsigned> cells;   // ncells + 1 (CSR offsets)
     std::vector<uint2> ranges;     // per cell [cells[c], cells[c + 1]): the device's view
@@ -23,7 +70,12 @@ struct GridHost {
     std::vector<int> rid, bid;
     int nx = 0, ny = 0, nz = 0;
     float lo[3] = {0, 0, 0}, h[3] = {1, 1, 1}, ih[3] = {1, 1, 1};
-    float pad = 0, errk = 0, ext = 0;
+    float pad = 0, ext = 0;
+    // exactness reach (GridView): the walk alone is exact for |o| <= reach_near; up to a
+    // distance (GridFarT) for |o| <= reach_dda
+    double reach_near = 0, reach_dda = 0;
+    float clo[3] = {0, 0, 0}, chi[3] = {0, 0, 0};   // the walked spheres' centre box
+    float f2near = 0, o2dda = 0, tsafe = 0, conea = 0, coneb = 0;
     int count = 0;
     // build statistics (the policy)
     double mean_refs = 0;   // references per non-empty cell
@@ -32,6 +84,14 @@ struct GridHost {
 
 // s: the scene (center, radius); sph: its device form float4(center, r^2); density: cells per
 // sphere of the box (more cells: fewer spheres per cell, more cell steps per ray).
+// The pad serves candidates up to kGridSafe scene radii from the origin (and the DDA origins
+// up to kGridDda), see the Padding note below.
+#ifndef LRT_GRID_SAFE
+#define LRT_GRID_SAFE 1.6
+#endif
+constexpr double kGridSafe = LRT_GRID_SAFE;
+constexpr double kGridDda = 8.0;
+
 inline void build_grid_at(const lrt_sphere* s, int n, const std::vector<float4>& sph, float density, GridHost& G) {
     G = GridHost();
     G.count = n;
@@ -130,9 +190,25 @@ inline void build_grid_at(const lrt_sphere* s, int n, const std::vector<float4>&
         ext = std::max(ext, std::max(std::fabs(lo[k]), std::fabs(hi[k])));
         span = std::max(span, hi[k] - lo[k]);
     }
-    // padding: far above the walk's rounding (2^-16 (|o| + ext) for origins up to ~8 scene
-    // sizes away, lrt_grid.h), far below a cell (~1/40 of the span)
-    const float pad0 = 1e-5f * ext + 2.5e-4f * span + 1e-6f;
+    // Padding, per sphere. Every hit point the reference computes must lie in its
+    // sphere's padded box, up to the DDA's rounding (below 2^-16 (max|o| + ext), lrt_grid.h).
+    // A candidate at distance t has |c - o| + r <= 1.004 t + 3.02 rmax <= Dsafe for t <= tsafe,
+    // so sphere i gets pad_i = hit_excursion(Dsafe, r_i) + the DDA's share for origins up to
+    // reach_dda: the walk then finds every candidate up to tsafe from any such origin, and
+    // every candidate at all from origins within reach_near = Dsafe - rs (|c - o| + r <= |o| +
+    // rs). tsafe is kGridSafe scene radii (rs); beyond it GridFarT / GridFinish take over.
+    double rs, rmin;
+    sphere_reach(s, in, rs, rmin);
+    double rmax = 0.0;
+    for (int i : in) rmax = std::max(rmax, (double)radii[i]);
+    const double tsafe = std::max(kGridSafe * rs, 1.0);
+    const double dsafe = 1.004 * tsafe + 3.02 * rmax;
+    const double reach_dda = kGridDda * rs + 1.0;
+    // the DDA's share: 2^-16 (|o| + ext) for |o| <= reach_dda, with the box's padded extent
+    // (ext grows by at most 2 pads, each far below the extent)
+    const double ddapad = std::ldexp(reach_dda + 1.01 * ext + 1e-3, -16);
+    auto pad_of = [&](double r) { return (float)((hit_excursion(dsafe, r) + ddapad) * (1.0 + 1e-6)); };
+    const float pad0 = std::max((float)(1e-5 * ext + 2.5e-4 * span + 1e-6), pad_of(rmin));   // the largest
     float e3[3];
     double vol = 1.0;
     for (int k = 0; k < 3; ++k) {
@@ -158,14 +234,26 @@ inline void build_grid_at(const lrt_sphere* s, int n, const std::vector<float4>&
     G.ext = 0.0f;
     for (int k = 0; k < 3; ++k) G.ext = std::max(G.ext, std::max(std::fabs(lo[k]), std::fabs(hi[k])));
     G.pad = pad0;
-    G.errk = 0.5f * pad0;
+    // near: |c - o| + r <= (the farthest corner of the centre box from o) + rmax <= dsafe
+    centre_box(s, in, G.clo, G.chi);
+    G.reach_near = std::max(0.0, dsafe - rmax);   // (a distance from the farthest corner)
+    G.reach_dda = std::max(reach_dda, G.reach_near + rs);
+    G.tsafe = (float)(tsafe * (1.0 - 1e-6));
+    G.f2near = reach_sq(G.reach_near);
+    G.o2dda = reach_sq(G.reach_dda);
+    {
+        const double c1 = std::sqrt(std::ldexp(1.0, -19)) + std::ldexp(24.0, -24);   // hit_excursion(D) <= c1 D
+        G.coneb = (float)(1.004 * c1 * (1.0 + 1.0 / 1024));
+        G.conea = (float)(3.02 * rmax * c1 * (1.0 + 1.0 / 1024));
+    }
     // cell lists (CSR), spheres in index order within a cell
     const long long ncells = (long long)nn[0] * nn[1] * nn[2];
     std::vector<unsigned> cnt(ncells + 1, 0u);
     auto range = [&](int i, int k, int& a, int& b) {
         const float c = k == 0 ? s[i].center.x : k == 1 ? s[i].center.y : s[i].center.z;
-        const float fa = (c - radii[i] - G.pad - G.lo[k]) * G.ih[k];
-        const float fb = (c + radii[i] + G.pad - G.lo[k]) * G.ih[k];
+        const float pi = std::min(G.pad, pad_of(radii[i]));   // (pad_of falls with r)
+        const float fa = (c - radii[i] - pi - G.lo[k]) * G.ih[k];
+        const float fb = (c + radii[i] + pi - G.lo[k]) * G.ih[k];
         a = std::max(0, std::min(nn[k] - 1, (int)std::floor(fa)));
         b = std::max(0, std::min(nn[k] - 1, (int)std::floor(fb)));
     };
@@ -228,9 +316,20 @@ inline GridView grid_view_host(const GridHost& G, const float4* all) {
     g.ihy = G.ih[1];
     g.ihz = G.ih[2];
     g.pad = G.pad;
-    g.errk = G.errk;
+    g.clox = G.clo[0];
+    g.cloy = G.clo[1];
+    g.cloz = G.clo[2];
+    g.chix = G.chi[0];
+    g.chiy = G.chi[1];
+    g.chiz = G.chi[2];
+    g.f2near = G.f2near;
+    g.o2dda = G.o2dda;
+    g.tsafe = G.tsafe;
+    g.conea = G.conea;
+    g.coneb = G.coneb;
     g.ext = G.ext;
     g.on = 1;
+    g.cells_refs = (unsigned)G.rsph.size();
     return g;
 }
 

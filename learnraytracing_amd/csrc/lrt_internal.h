@@ -33,6 +33,7 @@
 #include <vector>
 
 #include "lrt.h"
+#include "lrt_diag.h"
 #include "lrt_trace.h"
 
 #define LRT_VERSION_STRING "lrt-mi355x 0.3.0 gfx950"
@@ -203,9 +204,8 @@ struct Context {
     float4* d_bvh_nodes = nullptr;
     float4* d_bvh_lsph = nullptr;
     int* d_bvh_lid = nullptr;
-    float bvh_margin = 0.0f;
-    int bvh_nodes = 0;
-    int bvh_on = 0, bvh_big0 = 0, bvh_nbig = 0;
+    BvhView bvh{};   // geometry and the device pointers above (on: unused here)
+    int bvh_on = 0;
     int bvh_stack_levels = kBvhStackLevels;   // this scene's traversal depth (<= kBvhStackLevels)
     // uniform grid (the same scenes; lrt_grid.h): gv holds the device pointers and geometry,
     // gv.on = built; grid_pick = the policy's choice over the BVH (grid_suitable)
@@ -323,9 +323,12 @@ struct BvhHost {
     std::vector<int> lid;
     int big0 = 0, nbig = 0;
     float margin = 0.0f;
+    float clo[3] = {0, 0, 0}, chi[3] = {0, 0, 0};   // exactness reach (BvhView)
+    float f2near = 0.0f, rmax = 0.0f, rmin = 0.0f;
     int stack_levels = 1;   // traversal stack entries needed: one deferred sibling per level
 };
 void build_bvh_host(const lrt_sphere* s, int n, const std::vector<float4>& sph, BvhHost& out);
+void bvh_view_host(const BvhHost& B, BvhView& bv);   // the view of B's host arrays
 void free_scene(Context& c);
 int pack_scene(const lrt_sphere* s, const lrt_material* m, int n, std::vector<float4>& sph,
                std::vector<float4>& mats, std::vector<int>& lights);

@@ -313,14 +313,8 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
         }
         a.featMax = feat ? feat->max_frame : -1;
     }
-    a.bv.nodes = ctx().d_bvh_nodes;
-    a.bv.lsph = ctx().d_bvh_lsph;
-    a.bv.lid = ctx().d_bvh_lid;
-    a.bv.margin = ctx().bvh_margin;
+    a.bv = ctx().bvh;
     a.bv.on = (ctx().bvh_on && !(d->flags & LRT_F_NO_BVH)) ? 1 : 0;
-    a.bv.nnodes = ctx().bvh_nodes;
-    a.bv.big0 = ctx().bvh_big0;
-    a.bv.nbig = ctx().bvh_nbig;
     // the uniform grid where the scene suits it (grid_suitable; LRT_F_BVH / LRT_F_GRID force
     // one), except for feature launches (v0's BVH instances)
     a.gv = ctx().gv;

@@ -178,22 +178,42 @@ void build_bvh_host(const lrt_sphere* s, int n, const std::vector<float4>& sph, 
         const char* sd = getenv("LRT_BVH_SAH_DEPTH");
         if (sd) B.sahDepth = std::min(kBvhMaxBuildDepth, std::max(0, atoi(sd)));
     }
-    float extent = 1.0f;
+    std::vector<int> tree;
     for (int i = 0; i < n; ++i) {
         const bool finite = std::isfinite(s[i].center.x) && std::isfinite(s[i].center.y) &&
                             std::isfinite(s[i].center.z) && std::isfinite(radii[i]);
         // non-finite spheres have no box (and would break the split's ordering): like the
         // ground they are tested in index order by every ray, as in the reference's scan
-        if (!finite || (radii[i] > big_r && big.size() < 16)) {
-            big.push_back(i);
-            continue;
-        }
+        if (!finite || (radii[i] > big_r && big.size() < 16)) big.push_back(i);
+        else tree.push_back(i);
+    }
+    // Exactness: a box must hold every hit point the reference computes for its
+    // sphere, which can lie off the sphere by hit_excursion(|c - o| + r, r). Sphere i's box is
+    // padded by hit_excursion(dnear, r_i): enough for origins within dnear - rmax of every
+    // corner of the centre box (|c - o| + r <= that + rmax) -- as the grid's tsafe, 1.6 scene
+    // radii -- and a ray from anywhere else inflates each box it tests (MakeSlabRay).
+    double rs = 0.0, rmin = 0.0, rmax = 0.0;
+    sphere_reach(s, tree, rs, rmin);
+    for (int i : tree) rmax = std::max(rmax, (double)radii[i]);
+    const double dnear = 1.004 * std::max(kGridSafe * rs, 1.0) + 3.02 * rmax;
+    float clo[3], chi[3];
+    centre_box(s, tree, clo, chi);
+    out.clo[0] = clo[0], out.clo[1] = clo[1], out.clo[2] = clo[2];
+    out.chi[0] = chi[0], out.chi[1] = chi[1], out.chi[2] = chi[2];
+    out.f2near = reach_sq(std::max(0.0, dnear - rmax));
+    out.rmax = (float)(rmax * (1.0 + 1e-6));
+    out.rmin = (float)(rmin * (1.0 - 1e-6));
+    std::vector<float> xpad(n, 0.0f);
+    for (int i : tree) xpad[i] = (float)(hit_excursion(dnear, radii[i]) * (1.0 + 1e-6));
+    float extent = 1.0f;
+    for (int i : tree) {
         BvhPrim p;
         const float r = radii[i];
         const float c3[3] = {s[i].center.x, s[i].center.y, s[i].center.z};
         for (int k = 0; k < 3; ++k) {
-            // conservative box: c +/- |r|, padded well beyond float rounding
-            const float pad = 1e-5f * (std::fabs(c3[k]) + r) + 1e-6f;
+            // conservative box: c +/- |r|, padded well beyond float rounding and by the
+            // reference's hit excursion
+            const float pad = 1e-5f * (std::fabs(c3[k]) + r) + 1e-6f + xpad[i];
             p.lo[k] = c3[k] - r - pad;
             p.hi[k] = c3[k] + r + pad;
             p.c[k] = c3[k];
@@ -263,6 +283,27 @@ void build_bvh_host(const lrt_sphere* s, int n, const std::vector<float4>& sph, 
     out.margin = 1e-5f * extent + 1e-4f;
 }
 
+void bvh_view_host(const BvhHost& B, BvhView& bv) {
+    bv = BvhView{};
+    bv.nodes = B.nodes.data();
+    bv.lsph = B.lsph.data();
+    bv.lid = B.lid.data();
+    bv.margin = B.margin;
+    bv.on = 1;
+    bv.nnodes = (int)(B.nodes.size() / 8);
+    bv.big0 = B.big0;
+    bv.nbig = B.nbig;
+    bv.clox = B.clo[0];
+    bv.cloy = B.clo[1];
+    bv.cloz = B.clo[2];
+    bv.chix = B.chi[0];
+    bv.chiy = B.chi[1];
+    bv.chiz = B.chi[2];
+    bv.f2near = B.f2near;
+    bv.rmax = B.rmax;
+    bv.rmin = B.rmin;
+}
+
 void free_scene(Context& c) {
     if (c.d_bvh_nodes) (void)hipFree(c.d_bvh_nodes);
     if (c.d_bvh_lsph) (void)hipFree(c.d_bvh_lsph);
@@ -270,7 +311,7 @@ void free_scene(Context& c) {
     c.d_bvh_nodes = nullptr;
     c.d_bvh_lsph = nullptr;
     c.d_bvh_lid = nullptr;
-    c.bvh_nodes = 0;
+    c.bvh = BvhView{};
     c.bvh_on = 0;
     for (void* p : {(void*)c.d_grid_cells, (void*)c.d_grid_rsph, (void*)c.d_grid_rid, (void*)c.d_grid_bsph,
                     (void*)c.d_grid_bid})
@@ -351,10 +392,10 @@ int upload_scene(Context& c, const lrt_sphere* s, const lrt_material* m, int n) 
         LRT_HIP(upload(c.d_bvh_nodes, B.nodes));
         LRT_HIP(upload(c.d_bvh_lsph, B.lsph));
         LRT_HIP(upload(c.d_bvh_lid, B.lid));
-        c.bvh_nodes = (int)(B.nodes.size() / 8);
-        c.bvh_big0 = B.big0;
-        c.bvh_nbig = B.nbig;
-        c.bvh_margin = B.margin;
+        bvh_view_host(B, c.bvh);
+        c.bvh.nodes = c.d_bvh_nodes;
+        c.bvh.lsph = c.d_bvh_lsph;
+        c.bvh.lid = c.d_bvh_lid;
         c.bvh_stack_levels = B.stack_levels;
         c.bvh_on = 1;
     }
@@ -365,30 +406,12 @@ int upload_scene(Context& c, const lrt_sphere* s, const lrt_material* m, int n) 
         LRT_HIP(upload(c.d_grid_bsph, G.bsph));
         LRT_HIP(upload(c.d_grid_bid, G.bid));
         GridView& g = c.gv;
+        g = grid_view_host(G, c.d_sph);
         g.cells = c.d_grid_cells;
         g.rsph = c.d_grid_rsph;
         g.rid = c.d_grid_rid;
         g.bsph = c.d_grid_bsph;
         g.bid = c.d_grid_bid;
-        g.all = c.d_sph;
-        g.nbig = (int)G.bsph.size();
-        g.count = G.nx > 0 ? n : 0;
-        g.nx = G.nx;
-        g.ny = G.ny;
-        g.nz = G.nz;
-        g.lox = G.lo[0];
-        g.loy = G.lo[1];
-        g.loz = G.lo[2];
-        g.hx = G.h[0];
-        g.hy = G.h[1];
-        g.hz = G.h[2];
-        g.ihx = G.ih[0];
-        g.ihy = G.ih[1];
-        g.ihz = G.ih[2];
-        g.pad = G.pad;
-        g.errk = G.errk;
-        g.ext = G.ext;
-        g.on = 1;
         g.cells_refs = (unsigned)G.rsph.size();
         c.grid_pick = accel ? grid_suitable(G) : grid_forced();
     }

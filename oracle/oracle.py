@@ -91,8 +91,24 @@ def ref(n: int = 9):
         lib.ref_scatter.argtypes = [ctypes.c_int, _P, _P, ctypes.c_uint32, _P, _P, _P]
         lib.ref_draw_test.argtypes = [ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]
         lib.ref_initialize_threads.argtypes = [ctypes.c_int]
+        if hasattr(lib, "ref_hit_spheres_batch"):
+            lib.ref_hit_spheres_batch.argtypes = [_P, ctypes.c_int, _P, ctypes.c_int, _P, _P]
+            lib.ref_hit_spheres_batch.restype = None
         _refs[n] = lib
     return _refs[n]
+
+
+def ref_hit_spheres(rays, spheres):
+    """HitWorld's loop over an arbitrary sphere array with the reference's own HitSphere
+    (ref_harness.cpp ref_hit_spheres; parallel.cpp:54-73, maths.cpp:51-94). rays: (n, 6)
+    o.xyz, d.xyz (through the Ray ctor); spheres: (m, 4) center.xyz, radius.
+    Returns (ids int32, ts float32; t = 0 where nothing is hit)."""
+    rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 6)
+    spheres = np.ascontiguousarray(spheres, np.float32).reshape(-1, 4)
+    ids = np.zeros(len(rays), np.int32)
+    ts = np.zeros(len(rays), np.float32)
+    ref(9).ref_hit_spheres_batch(_ptr(rays), len(rays), _ptr(spheres), len(spheres), _ptr(ids), _ptr(ts))
+    return ids, ts
 
 
 def ref_drawtest_rate(width, height, budget_s, threads):

@@ -195,6 +195,38 @@ int ref_hit_world(const float* o, const float* d, float tMin, float tMax, float*
     out[6] = h.t;
     return id;
 }
+// HitWorld's loop (parallel.cpp:54-73) over an arbitrary sphere array: the reference's own
+// HitSphere (maths.cpp:51-94) on each sphere in index order with the shrinking closestT,
+// for scenes other than the 9 static ones (the accelerated closest-hit structures' checks).
+// spheres: 4 floats each (center xyz, radius). Returns id or -1; out as ref_hit_sphere.
+int ref_hit_spheres(const float* o, const float* d, const float* spheres, int n, float tMin, float tMax,
+                    float* out) {
+    Ray r(float3(o[0], o[1], o[2]), float3(d[0], d[1], d[2]));
+    Hit tmp, h;
+    int id = -1;
+    float closestT = tMax;
+    for (int i = 0; i < n; ++i) {
+        const float* s = spheres + 4 * i;
+        if (HitSphere(r, Sphere(float3(s[0], s[1], s[2]), s[3]), tMin, closestT, tmp)) {
+            h = tmp;
+            closestT = tmp.t;
+            id = i;
+        }
+    }
+    if (id < 0) return -1;
+    out[0] = h.pos.x; out[1] = h.pos.y; out[2] = h.pos.z;
+    out[3] = h.normal.x; out[4] = h.normal.y; out[5] = h.normal.z;
+    out[6] = h.t;
+    return id;
+}
+// Batched form: n_rays rays (o.xyz, d.xyz each) -> ids[i], ts[i] (t = 0 when no hit).
+void ref_hit_spheres_batch(const float* rays, int n_rays, const float* spheres, int n, int* ids, float* ts) {
+    float out[7];
+    for (int i = 0; i < n_rays; ++i) {
+        ids[i] = ref_hit_spheres(rays + 6 * i, rays + 6 * i + 3, spheres, n, kMinT, kMaxT, out);
+        ts[i] = ids[i] >= 0 ? out[6] : 0.0f;
+    }
+}
 float ref_schlick(float c, float ri) { return schlick(c, ri); }
 int ref_refract(const float* v, const float* n, float nint, float* out) {
     float3 o;

@@ -14,19 +14,40 @@ from learnraytracing_amd import dist as D
 from learnraytracing_amd.renderer import Job, default_camera, make_camera
 
 
-def header_functions():
-    src = open(L.HEADER_PATH).read()
+def header_functions(path=None):
+    src = open(path or L.HEADER_PATH).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w]+\s*\**\s*(lrt_\w+)\s*\(", src, flags=re.M)))
 
 
+def exported_functions():
+    """The dynamic symbols the library defines under the lrt_ prefix."""
+    import shutil
+    import subprocess
+    nm = shutil.which("nm")
+    if nm is None:
+        pytest.skip("nm not available")
+    out = subprocess.run([nm, "-D", "--defined-only", L.LIB_PATH], capture_output=True, text=True).stdout
+    return sorted({ln.split()[-1] for ln in out.splitlines() if ln.split() and ln.split()[-1].startswith("lrt_")})
+
+
 def test_library_exports_every_declared_symbol():
-    names = header_functions()
-    assert len(names) >= 16
+    api, diag = header_functions(), header_functions(L.DIAG_HEADER_PATH)
+    assert len(api) >= 16 and len(diag) >= 5
     lib = L.lib()
-    for n in names:
+    for n in api + diag:
         assert hasattr(lib, n), n
-    assert set(names) == set(L.SIGNATURES), "ctypes signatures out of sync with include/lrt.h"
+    assert set(api + diag) == set(L.SIGNATURES), "ctypes signatures out of sync with include/lrt.h + lrt_diag.h"
+
+
+def test_exported_symbol_set_is_the_two_headers():
+    """The renderer API (include/lrt.h) holds no diagnostics; the library exports exactly the
+    renderer API plus the diagnostics of include/lrt_diag.h, nothing else under lrt_."""
+    api, diag = header_functions(), header_functions(L.DIAG_HEADER_PATH)
+    assert not set(api) & set(diag)
+    for n in api:
+        assert not re.search(r"_stats$|_eval(_|$)", n), f"diagnostic {n} in the renderer API"
+    assert exported_functions() == sorted(api + diag)
 
 
 def test_library_is_gfx950_code():

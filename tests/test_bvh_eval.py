@@ -1,4 +1,4 @@
-"""Closest hit through the BVH (lrt_bvh_eval) against the reference's own HitWorld
+"""Closest hit through the BVH (lrt_accel_eval, accel 1) against the reference's own HitWorld
 (parallel.cpp:54-73 over random_scene(1000, 1), oracle/_ref/libref1000.so), bit for bit
 in id and t: the host build of the per-lane traversal (CPU), the device per-lane traversal
 and the device packet traversal (GPU). The rays are coherent bundles (a wave of nearby
@@ -58,7 +58,7 @@ def lrt_hits(rays, mode):
     ids = np.zeros(len(rays), np.int32)
     ts = np.zeros(len(rays), np.float32)
     r = np.ascontiguousarray(rays.reshape(-1))
-    L.check(L.lib().lrt_bvh_eval(sa, len(sph), _ptr(r), len(rays), _ptr(ids), _ptr(ts), mode))
+    L.check(L.lib().lrt_accel_eval(sa, len(sph), _ptr(r), len(rays), 1, mode, _ptr(ids), _ptr(ts)))
     return ids, ts
 
 

@@ -35,8 +35,8 @@ dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
 cam = np.concatenate([np.repeat(eye[None], m, 0), dirs], 1).astype(np.float32)
 ids = np.zeros(m, np.int32)
 ts = np.zeros(m, np.float32)
-L.check(L.lib().lrt_bvh_eval(sa, n, cam.ctypes.data_as(ctypes.c_void_p), m, ids.ctypes.data_as(ctypes.c_void_p),
-                             ts.ctypes.data_as(ctypes.c_void_p), 0))
+L.check(L.lib().lrt_accel_eval(sa, n, cam.ctypes.data_as(ctypes.c_void_p), m, 1, 0,
+                               ids.ctypes.data_as(ctypes.c_void_p), ts.ctypes.data_as(ctypes.c_void_p)))
 hit = ids >= 0
 P = cam[hit, :3] + cam[hit, 3:] * ts[hit, None]
 N = P - C[ids[hit]]

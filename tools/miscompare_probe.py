@@ -8,7 +8,7 @@
 2. re-renders each differing pixel ALONE (a 1x1 window: same seeds, same arithmetic, but
    no other pixel in its wave) -- a pixel that is right alone and wrong in its tile points
    at cross-lane state (LDS stack slots, the packet traversal's wave-uniform stack);
-3. runs the BVH closest hit on the device (per lane and packet, lrt_bvh_eval modes 1/2)
+3. runs the BVH closest hit on the device (per lane and packet, lrt_accel_eval BVH modes 1/2)
    against the host build of the same traversal (mode 0) on 2^18 random and coherent rays.
 Prints one JSON line.
 """
@@ -68,8 +68,8 @@ def main():
     for mode in (0, 1, 2):
         ids = np.zeros(n, np.int32)
         ts = np.zeros(n, np.float32)
-        L.check(L.lib().lrt_bvh_eval(sa, len(sph), rr.ctypes.data_as(ctypes.c_void_p), n,
-                                     ids.ctypes.data_as(ctypes.c_void_p), ts.ctypes.data_as(ctypes.c_void_p), mode))
+        L.check(L.lib().lrt_accel_eval(sa, len(sph), rr.ctypes.data_as(ctypes.c_void_p), n, 1, mode,
+                                       ids.ctypes.data_as(ctypes.c_void_p), ts.ctypes.data_as(ctypes.c_void_p)))
         res[mode] = (ids, ts)
     dev_mis = {m: int(((res[m][0] != res[0][0]) | (res[m][1].view(np.uint32) != res[0][1].view(np.uint32))).sum())
                for m in (1, 2)}
