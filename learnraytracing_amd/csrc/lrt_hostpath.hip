@@ -128,7 +128,7 @@ bool host_pipeline(const lrt_render_desc* d, size_t bytes) {
     }();
     // (an accelerated scene: the BVH, or the grid where render_device would pick it)
     const bool bvh = !(d->flags & LRT_F_NO_BVH) &&
-                     (ctx().bvh_on || (ctx().gv.on && (ctx().grid_pick || (d->flags & LRT_F_GRID))));
+                     (ctx().bvh_on || (ctx().grid_ok && (ctx().grid_pick || (d->flags & LRT_F_GRID))));
     const bool lds = !(d->flags & LRT_F_SCENE_GLOBAL) &&
                      sizeof(float4) * (kTraceLdsLevels * kBlock + 4 * (size_t)ctx().count + ctx().nlights / 4 + 1) <=
                          64 * 1024;

@@ -205,7 +205,8 @@ struct Context {
     float4* d_bvh_lsph = nullptr;
     int* d_bvh_lid = nullptr;
     BvhView bvh{};   // geometry and the device pointers above (on: unused here)
-    int bvh_on = 0;
+    int bvh_on = 0;            // the scene has more than kBvhMinSpheres spheres: the BVH applies
+    bool bvh_built = false;    // ... and has been built (ensure_bvh)
     int bvh_stack_levels = kBvhStackLevels;   // this scene's traversal depth (<= kBvhStackLevels)
     // uniform grid (the same scenes; lrt_grid.h): gv holds the device pointers and geometry,
     // gv.on = built; grid_pick = the policy's choice over the BVH (grid_suitable)
@@ -216,6 +217,8 @@ struct Context {
     int* d_grid_bid = nullptr;
     GridView gv{};
     bool grid_pick = false;
+    bool grid_ok = false;      // any scene: the grid applies (LRT_F_GRID below kBvhMinSpheres)
+    bool grid_built = false;   // ... and has been built (ensure_grid); gv.on then
 
     float* d_frame = nullptr;   // lrt_draw_test / lrt_render_host staging
     float4* d_col = nullptr;    // the pipelined host path's sample colours
@@ -333,6 +336,8 @@ void free_scene(Context& c);
 int pack_scene(const lrt_sphere* s, const lrt_material* m, int n, std::vector<float4>& sph,
                std::vector<float4>& mats, std::vector<int>& lights);
 int upload_scene(Context& c, const lrt_sphere* s, const lrt_material* m, int n);
+int ensure_bvh(Context& c);    // the structures on first use (lazy builds)
+int ensure_grid(Context& c);
 int camera_make(lrt_float3 lookFrom, lrt_float3 lookAt, lrt_float3 vup, float vfov, float aspect, float aperture,
                 float focusDist, lrt_camera* out);
 int camera_default(int w, int h, lrt_camera* out);

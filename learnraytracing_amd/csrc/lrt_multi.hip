@@ -38,13 +38,17 @@ int render_host_multi_enqueue(const lrt_render_desc* d, float* buf, size_t bytes
 int render_host_multi(const lrt_render_desc* d, float* buf, size_t bytes, long long* out_rays) {
     const int rc = render_host_multi_enqueue(d, buf, bytes);
     long long total = 0;
-    for (int k = 0; k < g_ndev; ++k) {   // also after a failure: nothing may still write the counters
+    hipError_t first = hipSuccess;
+    // every device's stream, also after a failure (advisor r4): nothing may still write the
+    // counters or DMA to or from the caller's buffer once render_host unlocks it
+    for (int k = 0; k < g_ndev; ++k) {
         DeviceScope ds(k);
         const hipError_t e = hipStreamSynchronize(ctx().stream);
-        if (e != hipSuccess && rc == LRT_OK) return hip_fail(e, "hipStreamSynchronize(multi-device render)");
+        if (e != hipSuccess && first == hipSuccess) first = e;
         total += (long long)*ctx().h_rays;
     }
     if (rc) return rc;
+    if (first != hipSuccess) return hip_fail(first, "hipStreamSynchronize(multi-device render)");
     snprintf(g_last_launch + strlen(g_last_launch), sizeof(g_last_launch) - strlen(g_last_launch),
              " devices=%d exchange=%s row_block=%d", g_ndev,
              !g_multi.gather ? "direct" : g_multi.rccl ? "rccl" : "copy", g_multi.row_block);

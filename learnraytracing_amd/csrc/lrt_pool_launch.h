@@ -34,10 +34,24 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     const size_t bstk = acc == kAccBvh ? sizeof(unsigned short) * ctx().bvh_stack_levels * 64
                         : acc == kAccGrid ? (sizeof(float4) + sizeof(int)) * (size_t)a.gv.nbig : 0;
     size_t grid_b = 0;
-    const int wpb = acc == kAccGrid && !lds
-                        ? pool_grid_wpb(a, sizeof(float4) * pool_lds_levels<kW>() * 64,
-                                        kPowTableBytes + (bstk + 15) / 16 * 16, &grid_b)
-                        : 1;
+    int wpb = acc == kAccGrid && !lds
+                  ? pool_grid_wpb(a, sizeof(float4) * pool_lds_levels<kW>() * 64,
+                                  kPowTableBytes + (bstk + 15) / 16 * 16, &grid_b)
+                  : 1;
+    if (wpb > 1) {
+        // dynamic LDS above the default limit: raised once per device for this instance
+        // (advisor r4: per device, and a refusal falls back to one-wave blocks)
+        static signed char raised[kMaxDevices * 4] = {};   // 0 not yet, 1 raised, -1 refused
+        int dev = 0, maxb = 0;
+        signed char* r = hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kMaxDevices * 4 ? &raised[dev] : nullptr;
+        if (r && *r == 0)
+            *r = hipDeviceGetAttribute(&maxb, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) == hipSuccess &&
+                         hipFuncSetAttribute((const void*)pool_kernel<MAXD, false, kAccGrid, kPix, 0, kW>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, maxb) == hipSuccess
+                     ? 1
+                     : -1;
+        if (!r || *r < 0) wpb = 1;
+    }
     const int lv = wpb > 1 ? pool_lds_levels<kW>() : kTraceLdsLevels;   // recursion stack levels in LDS
     const size_t stack = sizeof(float4) * lv * 64 * wpb + kPowTableBytes + (acc ? 0 : kRenormBytes);
     const size_t scene = lds ? sizeof(float4) * (4 * (size_t)a.count + (size_t)(a.nlights + 3) / 4 + 1) : 0;
@@ -54,16 +68,6 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
                           : lds ? (const void*)pool_kernel<MAXD, true, kAccScan, kPix>
                                 : (const void*)pool_kernel<MAXD, false, kAccScan, kPix>);
     int per_cu = 0;
-    if (wpb > 1) {   // dynamic LDS above the default limit (once per instance: the device's maximum)
-        static bool raised = false;
-        if (!raised) {
-            int dev = 0, maxb = 0;
-            if (hipGetDevice(&dev) == hipSuccess &&
-                hipDeviceGetAttribute(&maxb, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) == hipSuccess)
-                (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, maxb);
-            raised = true;
-        }
-    }
     hipError_t e = occupancy(&per_cu, kern, 64 * wpb, ldsb);
     if (e != hipSuccess) return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor");
     if (per_cu < 1) return fail(LRT_E_INVALID, "pool_kernel does not fit on a CU");

@@ -166,7 +166,12 @@ int pool_pixels(int frames, int xc, int rows) {
 // then the chunk's frame planes merged into the window. Path state is ~100 B + 16 B per
 // recursion level per pixel-sample; chunks are sized to a 2 GB budget.
 int launch_wavefront(KernelArgs a, bool lds, hipStream_t s) {
-    a.gv.on = 0;   // the wavefront kernels trace through the BVH
+    if (a.gv.on && ctx().bvh_on) {   // the wavefront kernels trace through the BVH
+        if (int rc = ensure_bvh(ctx())) return rc;
+        a.bv = ctx().bvh;
+        a.bv.on = 1;
+    }
+    a.gv.on = 0;
     const int frames = a.frames, levels = std::max(1, a.maxDepth);
     const size_t npix = (size_t)a.xc * a.rows;
     const size_t per_path = 4 + 4 * 16 + 16 + 5 * 4 + 16 * (size_t)levels;
@@ -313,15 +318,20 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
         }
         a.featMax = feat ? feat->max_frame : -1;
     }
-    a.bv = ctx().bvh;
-    a.bv.on = (ctx().bvh_on && !(d->flags & LRT_F_NO_BVH)) ? 1 : 0;
     // the uniform grid where the scene suits it (grid_suitable; LRT_F_BVH / LRT_F_GRID force
-    // one), except for feature launches (v0's BVH instances)
+    // one), except for feature launches (v0's BVH instances); the BVH for the other scenes above
+    // kBvhMinSpheres; either built on first use
+    const bool use_grid = ctx().grid_ok && !(d->flags & LRT_F_NO_BVH) && !want_feat && !(d->flags & LRT_F_BVH) &&
+                          (ctx().grid_pick || (d->flags & LRT_F_GRID));
+    const bool use_bvh = ctx().bvh_on && !(d->flags & LRT_F_NO_BVH) && !use_grid;
+    if (use_grid)
+        if (int rc = ensure_grid(ctx())) return rc;
+    if (use_bvh)
+        if (int rc = ensure_bvh(ctx())) return rc;
+    a.bv = ctx().bvh;
+    a.bv.on = use_bvh ? 1 : 0;
     a.gv = ctx().gv;
-    a.gv.on = (ctx().gv.on && !(d->flags & LRT_F_NO_BVH) && !want_feat && !(d->flags & LRT_F_BVH) &&
-               (ctx().grid_pick || (d->flags & LRT_F_GRID)))
-                  ? 1
-                  : 0;
+    a.gv.on = use_grid ? 1 : 0;
     a.bvh_stack_offset = 0;
     const bool lds = !(d->flags & LRT_F_SCENE_GLOBAL) &&
                      sizeof(float4) * (kTraceLdsLevels * kBlock + 4 * (size_t)a.count + a.nlights / 4 + 1) <= 64 * 1024;

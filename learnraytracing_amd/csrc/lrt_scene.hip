@@ -313,6 +313,7 @@ void free_scene(Context& c) {
     c.d_bvh_lid = nullptr;
     c.bvh = BvhView{};
     c.bvh_on = 0;
+    c.bvh_built = false;
     for (void* p : {(void*)c.d_grid_cells, (void*)c.d_grid_rsph, (void*)c.d_grid_rid, (void*)c.d_grid_bsph,
                     (void*)c.d_grid_bid})
         if (p) (void)hipFree(p);
@@ -323,6 +324,8 @@ void free_scene(Context& c) {
     c.d_grid_bid = nullptr;
     c.gv = GridView{};
     c.grid_pick = false;
+    c.grid_ok = false;
+    c.grid_built = false;
     if (c.d_sph) (void)hipFree(c.d_sph);
     if (c.d_mats) (void)hipFree(c.d_mats);
     if (c.d_lights) (void)hipFree(c.d_lights);
@@ -364,57 +367,100 @@ hipError_t upload(T*& d, const std::vector<T>& h) {   // a device copy (at least
     return e;
 }
 
-// Builds everything on the host first and checks it, then replaces the device's scene: a
-// refused scene leaves the previous one in place, whole (advisor r3: the BVH depth check used
-// to fail after the old scene was freed).
+// The BVH's and the grid's device copies (upload_scene, or later on first use: ensure_*).
+static int upload_bvh(Context& c, BvhHost& B) {
+    if (B.nodes.empty()) B.nodes.assign(4, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    LRT_HIP(upload(c.d_bvh_nodes, B.nodes));
+    LRT_HIP(upload(c.d_bvh_lsph, B.lsph));
+    LRT_HIP(upload(c.d_bvh_lid, B.lid));
+    bvh_view_host(B, c.bvh);
+    c.bvh.nodes = c.d_bvh_nodes;
+    c.bvh.lsph = c.d_bvh_lsph;
+    c.bvh.lid = c.d_bvh_lid;
+    c.bvh_stack_levels = B.stack_levels;
+    c.bvh_built = true;
+    return LRT_OK;
+}
+static int upload_grid(Context& c, const GridHost& G) {
+    LRT_HIP(upload(c.d_grid_cells, G.ranges));
+    LRT_HIP(upload(c.d_grid_rsph, G.rsph));
+    LRT_HIP(upload(c.d_grid_rid, G.rid));
+    LRT_HIP(upload(c.d_grid_bsph, G.bsph));
+    LRT_HIP(upload(c.d_grid_bid, G.bid));
+    GridView& g = c.gv;
+    g = grid_view_host(G, c.d_sph);
+    g.cells = c.d_grid_cells;
+    g.rsph = c.d_grid_rsph;
+    g.rid = c.d_grid_rid;
+    g.bsph = c.d_grid_bsph;
+    g.bid = c.d_grid_bid;
+    c.grid_built = true;
+    return LRT_OK;
+}
+static void pack_spheres(const std::vector<lrt_sphere>& s, std::vector<float4>& sph) {
+    sph.resize(s.size());
+    for (size_t i = 0; i < s.size(); ++i)
+        sph[i] = make_float4(s[i].center.x, s[i].center.y, s[i].center.z, s[i].radius * s[i].radius);
+}
+// The BVH is built when the policy picks it at lrt_set_scene, else on the first render that
+// asks for it (LRT_F_BVH, a feature launch, the wavefront kernels); the grid when the policy
+// needs it (scenes above kBvhMinSpheres, unless LRT_ACCEL=bvh), else on the first LRT_F_GRID
+// render. (advisor r4: every scene used to pay for both builds and both uploads.)
+int ensure_bvh(Context& c) {
+    if (c.bvh_built || !c.bvh_on) return LRT_OK;
+    std::vector<float4> sph;
+    pack_spheres(c.spheres, sph);
+    BvhHost B;
+    build_bvh_host(c.spheres.data(), c.count, sph, B);
+    if (B.stack_levels > kBvhStackLevels) return fail(LRT_E_INVALID, "BVH deeper than the traversal stack");
+    return upload_bvh(c, B);
+}
+int ensure_grid(Context& c) {
+    if (c.grid_built || !c.grid_ok) return LRT_OK;
+    std::vector<float4> sph;
+    pack_spheres(c.spheres, sph);
+    GridHost G;
+    build_grid_host(c.spheres.data(), c.count, sph, G);
+    return upload_grid(c, G);
+}
+
+// Builds what the policy needs on the host first and checks it, then replaces the device's
+// scene: a refused scene leaves the previous one in place, whole (advisor r3: the BVH depth
+// check used to fail after the old scene was freed).
 int upload_scene(Context& c, const lrt_sphere* s, const lrt_material* m, int n) {
     std::vector<float4> sph, mats;
     std::vector<int> lights;
     if (const int e = pack_scene(s, m, n, sph, mats, lights)) return e;
     const bool accel = n > kBvhMinSpheres;
+    const char* env = getenv("LRT_ACCEL");
+    const bool force_bvh = env && std::string(env) == "bvh";
     BvhHost B;
     GridHost G;
-    if (accel) {
+    bool have_grid = false, pick = false;
+    // the grid where the policy decides (grid_suitable) or is told to (LRT_ACCEL=grid)
+    if ((accel && !force_bvh) || (!accel && grid_forced())) {
+        build_grid_host(s, n, sph, G);
+        have_grid = true;
+        pick = accel ? grid_suitable(G) : true;
+    }
+    const bool have_bvh = accel && !pick;
+    if (have_bvh) {
         build_bvh_host(s, n, sph, B);
         // the LDS traversal stack is sized to B.stack_levels entries per lane, which bounds
         // every push (StackPush: at most one entry per level above the current node)
         if (B.stack_levels > kBvhStackLevels) return fail(LRT_E_INVALID, "BVH deeper than the traversal stack");
-        if (B.nodes.empty()) B.nodes.assign(4, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     }
-    // the grid for every scene: the default above kBvhMinSpheres where it suits the scene,
-    // opt-in below (LRT_F_GRID, LRT_ACCEL=grid)
-    if (n > 0) build_grid_host(s, n, sph, G);
     free_scene(c);
     LRT_HIP(upload(c.d_sph, sph));
     LRT_HIP(upload(c.d_mats, mats));
     LRT_HIP(upload(c.d_lights, lights));
-    if (accel) {
-        LRT_HIP(upload(c.d_bvh_nodes, B.nodes));
-        LRT_HIP(upload(c.d_bvh_lsph, B.lsph));
-        LRT_HIP(upload(c.d_bvh_lid, B.lid));
-        bvh_view_host(B, c.bvh);
-        c.bvh.nodes = c.d_bvh_nodes;
-        c.bvh.lsph = c.d_bvh_lsph;
-        c.bvh.lid = c.d_bvh_lid;
-        c.bvh_stack_levels = B.stack_levels;
-        c.bvh_on = 1;
-    }
-    if (n > 0) {
-        LRT_HIP(upload(c.d_grid_cells, G.ranges));
-        LRT_HIP(upload(c.d_grid_rsph, G.rsph));
-        LRT_HIP(upload(c.d_grid_rid, G.rid));
-        LRT_HIP(upload(c.d_grid_bsph, G.bsph));
-        LRT_HIP(upload(c.d_grid_bid, G.bid));
-        GridView& g = c.gv;
-        g = grid_view_host(G, c.d_sph);
-        g.cells = c.d_grid_cells;
-        g.rsph = c.d_grid_rsph;
-        g.rid = c.d_grid_rid;
-        g.bsph = c.d_grid_bsph;
-        g.bid = c.d_grid_bid;
-        g.cells_refs = (unsigned)G.rsph.size();
-        c.grid_pick = accel ? grid_suitable(G) : grid_forced();
-    }
+    c.bvh_on = accel ? 1 : 0;
+    c.grid_ok = n > 0;
+    c.grid_pick = pick;
+    if (have_bvh)
+        if (int rc = upload_bvh(c, B)) return rc;
+    if (have_grid)
+        if (int rc = upload_grid(c, G)) return rc;
     c.count = n;
     ++c.scene_version;
     c.nlights = (int)lights.size();
