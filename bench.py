@@ -38,6 +38,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -65,6 +66,55 @@ PMC_INDEX = os.path.join(ROOT, "profiles", "pmc_index.json")
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+class Watchdog:
+    """Bounds every phase of the run (the first multi-GPU run on the driver's 8-GPU node must
+    end in a diagnosable line, not a hung job): enter(name) starts a phase with its own time
+    limit (LRT_BENCH_TIMEOUT, seconds, default 600); when one expires on any rank, that rank
+    reports the phase on stderr and rank 0 prints a partial JSON line naming it (value null),
+    then the process exits with status 3. A rank blocked in a collective because a peer
+    stalled times out in its own phase, so rank 0 always reports. The thread only reads state
+    and prints; nothing is re-executed. LRT_BENCH_STALL=<phase> (tests) makes every rank, or
+    rank LRT_BENCH_STALL_RANK, hang at the start of that phase."""
+
+    def __init__(self, rank, world, base):
+        self.rank, self.world, self.base = rank, world, base
+        self.limit = float(os.environ.get("LRT_BENCH_TIMEOUT", "600"))
+        self.phase, self.deadline, self.started = "start", time.monotonic() + self.limit, time.monotonic()
+        self.done = []   # phases completed, in order
+        self.lock = threading.Lock()
+        self.stall = os.environ.get("LRT_BENCH_STALL")
+        self.stall_rank = os.environ.get("LRT_BENCH_STALL_RANK")
+        threading.Thread(target=self._run, name="bench-watchdog", daemon=True).start()
+
+    def enter(self, name, limit=None):
+        with self.lock:
+            if self.phase != "start":
+                self.done.append(self.phase)
+            self.phase = name
+            self.started = time.monotonic()
+            self.deadline = self.started + (limit or self.limit)
+        if self.stall == name and (self.stall_rank is None or int(self.stall_rank) == self.rank):
+            log(f"rank {self.rank}: LRT_BENCH_STALL={name}: hanging here")
+            while True:
+                time.sleep(3600)
+
+    def _run(self):
+        while True:
+            time.sleep(0.25)
+            with self.lock:
+                expired = time.monotonic() > self.deadline
+                phase, waited, done = self.phase, time.monotonic() - self.started, list(self.done)
+            if expired:
+                break
+        msg = f"timeout: phase '{phase}' ran {waited:.1f} s on rank {self.rank} of {self.world} (limit {self.limit:.0f} s)"
+        log(msg)
+        if self.rank == 0:
+            line = dict(self.base)
+            line.update({"value": None, "error": msg, "failed_phase": phase, "phases_completed": done})
+            print(json.dumps(line), flush=True)
+        os._exit(3)
 
 
 def workload(config: int, world: int = 1, scaling: str = "strong", spp=None, depth=None, shard_of: int = 1):
@@ -246,10 +296,16 @@ def main():
     cfg = workload(args.config, world, args.scaling, args.spp, args.depth, args.shard_of)
     cfg_name = f"config{args.config}"
     extra = not args.no_extra_legs
+    wd = Watchdog(rank, world, {
+        "metric": METRIC, "value": None, "unit": "Mray/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
+        "dtype": "f32", "data": "synthetic", "config": {"workload": f"{cfg_name}: {cfg['width']}x{cfg['height']}, "
+                                                                    f"{cfg['spp_total']} spp, {cfg['depth']} bounces"}})
 
     # CPU baselines first: rank 0 at N=1 only, before anything touches the GPU.
     cpu = cpu1 = cpu_dt = None
     if rank == 0 and world == 1 and extra and not args.no_cpu_baseline:
+        wd.enter("cpu_baseline")
         cores = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
         cores = max(1, min(cores, os.cpu_count() or 1))
         budget = args.cpu_budget if args.cpu_budget is not None else max(1.5, 15.0 / cores)
@@ -261,18 +317,25 @@ def main():
         if cpu_dt:
             log(f"reference DrawTest (enkiTS, {cores} threads): {cpu_dt['value']:.1f} Mray/s")
 
+    wd.enter("import_torch", max(wd.limit, 300.0))   # (a fresh box pages the image in: 1-2 minutes)
+    import datetime
+
     import torch
     import torch.distributed as dist
 
     backend = os.environ.get("LRT_DIST_BACKEND", "nccl")   # nccl = RCCL; gloo only to rehearse on 1 GPU
     # LRT_BENCH_SAME_GPU=1 puts every rank on GPU 0 (rehearsing the RCCL path on a 1-GPU box)
     gpu = 0 if (backend != "nccl" or os.environ.get("LRT_BENCH_SAME_GPU") == "1") else local_rank
-    torch.cuda.set_device(gpu)
-    if world > 1:
+    if world > 1:   # the rendezvous itself is bounded too (the store's timeout)
+        wd.enter("init_process_group")
+        tmo = datetime.timedelta(seconds=wd.limit * 1.5)   # (the watchdog reports first)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+            torch.cuda.set_device(gpu)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu), timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
+    wd.enter("device_init", max(wd.limit, 300.0))
+    torch.cuda.set_device(gpu)
     import learnraytracing_amd as lrt
     from learnraytracing_amd import _lib as L
     from learnraytracing_amd.dist import gather_to_root, max_shard_rows, open_shared_frames, shard_rows
@@ -311,11 +374,16 @@ def main():
     # --no-extra-legs): the fused remote stores, and north_star's RCCL gather over xGMI
     both = world > 1 and extra
     shared = None
+    ipc_refused = None
     if remote or both:
+        wd.enter("open_shared_frames")
         dev_b = dev if backend == "nccl" else torch.device("cpu")
-        shared = open_shared_frames(W, H, nslots, rank, dev_b)
+        # LRT_BENCH_FORCE_IPC_FAIL=1 (tests): every rank reports a refused mapping
+        shared = open_shared_frames(W, H, nslots, rank, dev_b,
+                                    force_fail=os.environ.get("LRT_BENCH_FORCE_IPC_FAIL") == "1")
         if shared is None:   # IPC mapping refused on some rank: the RCCL exchange instead
             log("note: IPC frame mapping failed on a rank; falling back to --exchange rccl")
+            ipc_refused = "lrt_ipc_open refused on at least one rank: the remote-store exchange was not run"
             remote = False
     have_rccl = world > 1 and (not remote or both)
     # the RCCL exchange carries RGB only (lrt_pack_rgb): 12 of the 16 bytes per pixel cross xGMI
@@ -394,12 +462,14 @@ def main():
 
     def timed(mode):
         """warmup + K timed steps of `mode`: (seconds, counted rays of this rank)."""
+        wd.enter(f"warmup_{mode}")
         for k in range(warmup):
             step(k, mode)
         drain()
         sync_all()
         rays.zero_()
         sync_all()
+        wd.enter(f"timed_{mode}")
         t0 = time.perf_counter()
         for k in range(args.steps):
             step(warmup + k, mode)
@@ -414,10 +484,24 @@ def main():
     elapsed, timed_rays = timed(mode)
     launch_info = L.last_launch()
     exchange_legs = None
+    if both and shared is None:   # the RCCL leg alone: the line still carries the exchange's timing
+        wd.enter("exchange_legs")
+        st = torch.tensor([elapsed, timed_rays], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        mx, sm = st.clone(), st.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        exchange_legs = {
+            "primary": mode, "frames_identical": None,
+            "legs": {"rccl": {"ms_per_step": round(float(mx[0]) / args.steps * 1e3, 4),
+                              "value": round(float(sm[1]) / float(mx[0]) / 1e6, 3), "unit": "Mray/s",
+                              "what": "pack to RGB + RCCL gather (dist.gather over nccl = RCCL) to rank 0 + unshard"},
+                     "remote": {"refused": ipc_refused}},
+        }
     if both and shared is not None:
         # the other exchange, same steps; then both legs' assembled frames, bit for bit, on rank 0
         other = "rccl" if mode == "remote" else "remote"
         e2, r2 = timed(other)
+        wd.enter("exchange_legs")
         legs = {mode: (elapsed, timed_rays), other: (e2, r2)}
         st = torch.tensor([legs["remote"][0], legs["rccl"][0], legs["remote"][1], legs["rccl"][1]],
                           dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
@@ -444,6 +528,7 @@ def main():
     alone_ms = e2e_s = None
     e2e_steps = 0
     if extra:
+        wd.enter("launch_alone")
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.steps)]
         scratch = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -460,6 +545,7 @@ def main():
             shape = (H, W, 4) if world > 1 else tuple(bufs[0].shape)   # --shard-of: the shard itself
             host = [torch.empty(shape, dtype=torch.float32, pin_memory=True) for _ in range(nslots)]
         e2e_steps = max(1, min(args.steps, 10))
+        wd.enter("end_to_end")
         if remote:   # a frame is complete once every rank's render of it is: barrier, then D2H
             def e2e_step(k):
                 step(k, mode)
@@ -491,6 +577,8 @@ def main():
     # ---- the reference API as its own caller uses it (rank 0, N = 1): DrawTest per frame, on
     # one device and split over two contexts of it (lrt_initialize_devices([0, 0]): the
     # multi-device host path's own cost, rehearsed on the one GPU this process drives)
+    if extra and world == 1:
+        wd.enter("drawtest")
     drawtest = drawtest_leg(lrt) if extra and world == 1 else None
     drawtest_multi = None
     if extra and world == 1:
@@ -503,6 +591,7 @@ def main():
         lrt.InitializeTest()
     torch.cuda.synchronize()
 
+    wd.enter("stats")
     stats = torch.tensor([elapsed, timed_rays, alone_ms or 0.0, e2e_s or 0.0], dtype=torch.float64,
                          device=dev if backend == "nccl" else "cpu")
     if world > 1:
@@ -622,6 +711,7 @@ def main():
             "exchange": exchange_legs,
         }
         print(json.dumps(out), flush=True)
+    wd.enter("teardown")
     if rstream is not None:
         torch.cuda.set_stream(torch.cuda.default_stream(dev))
         rstream.close()

@@ -150,18 +150,22 @@ class _CudaArray:
                                          "version": 3, "strides": None}
 
 
-def open_shared_frames(width: int, height: int, count: int, rank: int, device, group=None):
+def open_shared_frames(width: int, height: int, count: int, rank: int, device, group=None, force_fail=False):
     """SharedFrames on every rank, or None on every rank when any rank fails to allocate or
     map them (the ranks agree through one all-reduce), so the caller can fall back to the
-    RCCL exchange instead of one rank dying while the others wait in a collective."""
+    RCCL exchange instead of one rank dying while the others wait in a collective.
+    force_fail: this rank reports a refused mapping without trying (tests of the fallback)."""
     import torch
     import torch.distributed as dist
 
     frames, err = None, None
-    try:
-        frames = SharedFrames(width, height, count, rank, group=group)
-    except Exception as e:
-        err = e
+    if force_fail:
+        err = RuntimeError("IPC mapping refused (forced)")
+    else:
+        try:
+            frames = SharedFrames(width, height, count, rank, group=group)
+        except Exception as e:
+            err = e
     if not dist.is_initialized():
         if err is not None:
             raise err

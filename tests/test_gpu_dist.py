@@ -184,6 +184,26 @@ def test_bench_two_ranks_gloo(gpu, scaling, exchange):
     assert set(ex["legs"]) == {"remote", "rccl"} and all(v["value"] > 0 for v in ex["legs"].values()), ex
 
 
+def test_bench_two_ranks_ipc_refused(gpu):
+    """The driver's N > 1 line when IPC mapping is refused on a rank (LRT_BENCH_FORCE_IPC_FAIL):
+    the run falls back to the RCCL exchange and the line still carries its timed leg, with the
+    remote leg marked refused -- never a line without exchange legs."""
+    env = dict(os.environ, LRT_DIST_BACKEND="gloo", LRT_BENCH_FORCE_IPC_FAIL="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = lines[0]
+    assert d["value"] > 0 and d["config"]["rays_per_step"] == 11669343
+    ex = d["exchange"]
+    assert ex["primary"] == "rccl" and ex["legs"]["rccl"]["value"] > 0, ex
+    assert "refused" in ex["legs"]["remote"] and ex["legs"]["remote"]["refused"], ex
+    assert "RCCL gather" in d["config"]["parallelism"]
+
+
 @pytest.mark.parametrize("kernel,scene", [("pool", "default"), ("wavefront", "default"), ("pool", "scene1000"),
                                           ("v0", "scene1000"), ("pool-bvh", "scene1000")])
 def test_fused_frame_store_every_kernel(gpu, kernel, scene):
