@@ -110,6 +110,8 @@ class Watchdog:
                 break
         msg = f"timeout: phase '{phase}' ran {waited:.1f} s on rank {self.rank} of {self.world} (limit {self.limit:.0f} s)"
         log(msg)
+        if self.rank != 0:   # rank 0 reports first: the launcher stops every rank once one has exited
+            time.sleep(min(10.0, self.limit))
         if self.rank == 0:
             line = dict(self.base)
             line.update({"value": None, "error": msg, "failed_phase": phase, "phases_completed": done})

@@ -34,15 +34,11 @@ int init_context(Context& c, int dev) {
     // not queue behind one another: created lazily, between other streams, they did on some
     // offsets -- a pageable DrawTest at 1280x720 took 0.67-0.77 ms/frame instead of 0.49-0.52
     // (tools/drawtest_queues.py, profiles/r4_m); a high-priority queue is one no stream of normal
-    // priority shares. LRT_STREAM_PRIO: 1 (default) as described, 0 all at normal priority.
+    // priority shares.
     {
-        static const int prio_mode = [] {
-            const char* e = getenv("LRT_STREAM_PRIO");
-            return e ? atoi(e) : 1;
-        }();
         int least = 0, greatest = 0;
         LRT_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        LRT_HIP(hipStreamCreateWithPriority(&c.stream, hipStreamNonBlocking, prio_mode >= 1 ? greatest : least));
+        LRT_HIP(hipStreamCreateWithPriority(&c.stream, hipStreamNonBlocking, greatest));
         LRT_HIP(hipStreamCreateWithPriority(&c.s_in, hipStreamNonBlocking, least));
     }
     if (int rc = create_lookahead_stream(c)) return rc;

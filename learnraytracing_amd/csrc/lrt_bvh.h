@@ -343,17 +343,10 @@ LRT_DEV bool ShadowReachesLightBVH4(const F3& o, const F3& d, int li, const floa
 // queries in registers across the shading code 82 VGPRs spilled (config 4: 404-829 ms
 // instead of 226); with the queries saved to memory between a traversal phase and a
 // shading phase still 90 spilled (371-583 ms instead of 224).
-// LRT_TRAV_UNROLL: unroll factor of TravStep's loop over a node's 4 children (A/B).
-#ifndef LRT_TRAV_UNROLL
-#define LRT_TRAV_UNROLL 4
-#endif
-// LRT_TRAV_FLAT_LEAVES: the spheres of all leaf children a lane hits in a node are tested in
-// one loop after the box tests (a wave runs max over lanes of their sum) instead of one loop
-// per child slot inside the box-test loop (the sum over slots of each slot's max). Leaf
-// positions must fit 12 bits and counts 1..16 (LRT_MAX_SPHERES <= 4096, leaves <= 16).
-#ifndef LRT_TRAV_FLAT_LEAVES
-#define LRT_TRAV_FLAT_LEAVES 1
-#endif
+// The spheres of all leaf children a lane hits in a node are tested in one loop after the box
+// tests (a wave runs max over lanes of their sum), not one loop per child slot inside the
+// box-test loop. Leaf positions must fit 12 bits and counts 1..16 (LRT_MAX_SPHERES <= 4096,
+// leaves <= 16).
 struct TravQuery {
     F3 o, d, db;   // origin, the current query's direction, the bounce ray's direction
     SlabRay sr;    // of d
@@ -427,8 +420,8 @@ LRT_DEV void TravStep(TravQuery& q, const BvhView& bv, unsigned short* stk, int 
         const float mbase = bv.margin + q.sr.mo;
         int next = -1, rem = 0, nextRef = 0;
         float nearT = __builtin_inff();
-        uint32_t lmask = 0, lpack0 = 0, lpack1 = 0;   // LRT_TRAV_FLAT_LEAVES: the node's leaves hit
-#pragma unroll LRT_TRAV_UNROLL
+        uint32_t lmask = 0, lpack0 = 0, lpack1 = 0;   // the node's leaves this lane hit
+#pragma unroll
         for (int c = 0; c < 4; ++c) {
             if (!((q.msk >> c) & 1)) continue;
             const float4 lo = bv.nodes[8 * q.cur + 2 * c], hi = bv.nodes[8 * q.cur + 2 * c + 1];
@@ -441,14 +434,11 @@ LRT_DEV void TravStep(TravQuery& q, const BvhView& bv, unsigned short* stk, int 
             if (!(tn <= __builtin_fminf(tfm, q.bestT + mb) && tfm >= kMinT)) continue;
             if (cnt > 0) {
                 const int ref = lrt::libm::f2u_i(lo.w);
-                if (LRT_TRAV_FLAT_LEAVES) {   // leaf position (12 bits) and count - 1 (4 bits)
-                    const uint32_t e = (uint32_t)ref | ((uint32_t)(cnt - 1) << 12);
-                    if (c < 2) lpack0 |= e << (16 * c);
-                    else lpack1 |= e << (16 * (c - 2));
-                    lmask |= 1u << c;
-                } else {
-                    for (int j = 0; j < cnt; ++j) TravTest(q, bv, ref + j, bv.lsph[ref + j]);
-                }
+                // leaf position (12 bits) and count - 1 (4 bits)
+                const uint32_t e = (uint32_t)ref | ((uint32_t)(cnt - 1) << 12);
+                if (c < 2) lpack0 |= e << (16 * c);
+                else lpack1 |= e << (16 * (c - 2));
+                lmask |= 1u << c;
             } else {
                 rem |= 1 << c;
                 if (tn < nearT) {
@@ -458,7 +448,7 @@ LRT_DEV void TravStep(TravQuery& q, const BvhView& bv, unsigned short* stk, int 
                 }
             }
         }
-        if (LRT_TRAV_FLAT_LEAVES) {   // one loop over the spheres of every leaf this lane hit
+        {   // one loop over the spheres of every leaf this lane hit
             int cs = lmask ? __builtin_ctz(lmask) : 0, jj = 0;
             while (lmask) {
                 const uint32_t e = ((cs < 2 ? lpack0 >> (16 * cs) : lpack1 >> (16 * (cs - 2)))) & 0xFFFFu;
@@ -525,11 +515,9 @@ LRT_DEV int ClosestHitDualBVH4(const F3& o, const F3& db, bool hasS, const F3& d
 // Exactness is unchanged: a lane tests every sphere its own conservative culling keeps (a
 // superset is harmless -- the (cand, index) minimum over more real spheres is the same),
 // with the same per-sphere arithmetic. Device only; the caller checks that every active
-// lane has the FMA slab form. LRT_PACKET_DEPTH: scatter events below which a path's rays
-// go this way (0: never).
-#ifndef LRT_PACKET_DEPTH
-#define LRT_PACKET_DEPTH 1
-#endif
+// lane has the FMA slab form. kPacketDepth: scatter events below which a path's rays go this
+// way (v0: a path's first rays).
+constexpr int kPacketDepth = 1;
 #if defined(__HIP_DEVICE_COMPILE__)
 #define LRT_PACKET_AVAILABLE 1
 typedef const __attribute__((address_space(4))) float4* CF4Ptr;

@@ -27,6 +27,20 @@
 
 namespace lrt {
 
+// Exactness reach (lrt_grid_build.h): an origin within sqrt(f2near) of every corner
+// of the grid's box: the walk alone is exact; otherwise, with dot(o, o) <= o2dda, the walk is
+// exact up to tsafe from o, and a ray whose candidates could lie farther (GridFarClear) scans
+// every sphere at the end unless its answer came first; beyond (or NaN): the scan. In memory,
+// not in the view: read at each use (grid_reach), the values hold no registers across the walk
+// (held in the view they added ~30 B of spills per lane to the pool kernel's grid instance).
+struct GridReach {
+    float f2near, o2dda;
+    float tsafe;   // the walk finds every candidate up to tsafe from such an origin
+    float conea;   // a reference hit point at t lies within conea + kConeB t of the box (plus
+                   // GridFarClear's rounding slack)
+    float lo[3], hi[3];   // the grid's box, as GridPlane gives it
+};
+
 struct GridView {
     const uint2* cells;      // per cell: [start, end) of its spheres in rsph / rid
     const float4* rsph;      // cell-ordered sphere copies: float4(center, r^2)
@@ -40,22 +54,14 @@ struct GridView {
     float hx, hy, hz;        // cell size per axis
     float ihx, ihy, ihz;     // 1 / cell size
     float pad;               // insertion padding (absolute)
-    // exactness reach (lrt_grid_build.h): an origin within sqrt(f2near) of every
-    // corner of the walked spheres' centre box (clo, chi): the walk alone is exact; otherwise,
-    // with dot(o, o) <= o2dda, the walk is exact up to tsafe from o, and a ray whose candidates
-    // could lie farther (GridFarT) scans every sphere at the end unless its answer came first;
-    // beyond (or NaN): the scan
-    float clox, cloy, cloz, chix, chiy, chiz;
-    float f2near, o2dda;
-    float tsafe;             // the walk finds every candidate up to tsafe from such an origin
-    float conea, coneb;      // a reference hit point at t lies within conea + coneb t of the box
+    const struct GridReach* reach;   // exactness reach (GridReach), read where used
     float ext;               // max |coordinate| of the box
     int on;
-    unsigned cells_refs;     // entries of rsph / rid (the LDS copy's size, LRT_POOL_GRID_WPB)
+    unsigned cells_refs;     // entries of rsph / rid (the LDS copy's size, kPoolGridWaves blocks)
 };
 
 // The walk's reads of the cell ranges and the cell-ordered spheres. kL = 1: the pool kernel's
-// block-shared LDS copy (LRT_POOL_GRID_WPB): the view's pointers are generic addresses of
+// block-shared LDS copy (kPoolGridWaves blocks): the view's pointers are generic addresses of
 // that copy, read here as LDS (ds_read instead of flat loads). Any other reader of the same
 // view (the other lights' shadow queries) goes through the generic pointers.
 template <class T>
@@ -82,9 +88,9 @@ struct GridQuery {
     int best, li;
     int cx, cy, cz;   // current cell
     unsigned j, jend; // the current cell's sphere range still to test
-    float farT;       // the scan is needed at the end unless bestT < farT (+inf: never)
     int mode;         // 0 walking, 2 this query is over
     bool sh, lit, busy;
+    bool far;         // the walk's answer is certain only up to tsafe (GridStart, GridFinish)
 };
 
 LRT_DEV float GridPlane(float lo, int c, float h) { return lo + (float)c * h; }
@@ -110,43 +116,74 @@ LRT_DEV void GridTest(GridQuery& q, const float4& s, int id, bool on = true) {  
     q.best = w ? id : q.best;
 }
 
-// For a ray from beyond the grid's near reach (o2near < |o|^2 <= o2dda) the walk finds every
+LRT_DEV GridReach grid_reach(const GridView& g) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(4))) GridReach* P;   // (uniform: scalar loads)
+    const unsigned long long v = (unsigned long long)g.reach;
+    unsigned long long u = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(v >> 32)) << 32) |
+                           (unsigned)__builtin_amdgcn_readfirstlane((unsigned)v);
+    asm volatile("" : "+s"(u));   // loaded here, each time: not hoisted into the loop's registers
+    return *(P)u;
+#else
+    return *g.reach;
+#endif
+}
+
+// hit_excursion(D) <= c1 D (c1 = 2^-9.5 + 24 2^-24) with D <= 1.004 t + 3.02 rmax: the cone's
+// slope, 1.004 c1 (1 + 2^-10) (lrt_grid_build.h checks it)
+constexpr float kConeB = 0.00139f;
+
+// For a ray from beyond the grid's near reach (but within o2dda) the walk finds every
 // candidate up to tsafe (the padding is sized for them, lrt_grid_build.h). A candidate beyond
-// lies within conea + coneb t of the grid's box (hit_excursion <= c1 D, D <= 1.004 t + 3.02 r),
-// a cone around the box: the t interval in which the ray is inside it is an intersection of 6
-// half-lines. Returns the t from which the walk's answer is not certain (less a margin), or
-// +inf when the cone beyond tsafe is empty. Conservative throughout; few rays come here.
-LRT_DEV float rcp_approx(float x) {   // within 1 ulp of 1 / x (v_rcp_f32); exact on the host
-#if defined(__HIP_DEVICE_COMPILE__)
-    return __builtin_amdgcn_rcpf(x);
-#else
-    return 1.0f / x;
-#endif
-}
-LRT_DEV float sqrt_approx(float x) {   // within 1 ulp (v_sqrt_f32)
-#if defined(__HIP_DEVICE_COMPILE__)
-    return __builtin_amdgcn_sqrtf(x);
-#else
-    return __builtin_sqrtf(x);
-#endif
-}
-LRT_DEV float GridFarT(const GridQuery& q, const GridView& g, float o2) {
-    const float a = g.conea + (sqrt_approx(o2) * 1.0000019073486328125f + g.ext) * 1.52587890625e-05f, b = g.coneb;
-    float tA = 0.0f, tB = __builtin_inff();
-    auto axis = [&](float o, float d, float lo, float hi) {
-        // lo - a - b t <= o + t d <= hi + a + b t:  (d + b) t >= lo - a - o,  (d - b) t <= hi + a - o
-        const float dp = d + b, dm = d - b, r1 = lo - a - o, r2 = hi + a - o;
-        const float q1 = r1 * rcp_approx(dp), q2 = r2 * rcp_approx(dm);   // (1 ulp: inside the slack)
-        tA = dp > 0.0f ? __builtin_fmaxf(tA, q1) : tA;
-        tB = dp < 0.0f ? __builtin_fminf(tB, q1) : ((dp == 0.0f) & (r1 > 0.0f)) ? -1.0f : tB;
-        tB = dm > 0.0f ? __builtin_fminf(tB, q2) : ((dm == 0.0f) & (r2 < 0.0f)) ? -1.0f : tB;
-        tA = dm < 0.0f ? __builtin_fmaxf(tA, q2) : tA;
+// lies within conea + kConeB t of the grid's box (conea also holds the rounding slack of the
+// test below): a cone around the box. Is the ray outside it for every t >= tsafe? It is when,
+// on some axis, it is beyond the cone's slab at tsafe and moves away from it at least as fast
+// as the slab widens. No division, few registers (this runs in the pool kernel's loop, where
+// the walk's state is live: the exact cone interval, 6 reciprocals, added ~56 B of spills).
+LRT_DEV bool GridFarClear(const GridQuery& q, const GridView& g, const GridReach& R) {
+    const float a = R.conea, b = kConeB, t = R.tsafe;
+    // per axis: moving away from the far side at |d| - b >= 0 and beyond it at tsafe
+    auto away = [&](float o, float d, float lo, float hi) {
+        const float m = d > 0.0f ? o - hi : lo - o;
+        const float e = __builtin_fabsf(d) - b;
+        return (e >= 0.0f) & (m - a + t * e > 0.0f);
     };
-    axis(q.o.x, q.d.x, g.lox, GridPlane(g.lox, g.nx, g.hx));
-    axis(q.o.y, q.d.y, g.loy, GridPlane(g.loy, g.ny, g.hy));
-    axis(q.o.z, q.d.z, g.loz, GridPlane(g.loz, g.nz, g.hz));
-    const float lo = __builtin_fmaxf(tA, g.tsafe);
-    return lo < tB * 1.0000152587890625f + g.pad ? lo * 0.9999847412109375f - g.pad : __builtin_inff();
+    (void)g;
+    return away(q.o.x, q.d.x, R.lo[0], R.hi[0]) | away(q.o.y, q.d.y, R.lo[1], R.hi[1]) | away(q.o.z, q.d.z, R.lo[2], R.hi[2]);
+}
+
+// Is o within sqrt(f2near) of every corner of the grid's box, which holds every walked
+// sphere's centre (then every candidate's |c - o| + r stays within the distance the padding
+// serves)? False for NaN.
+LRT_DEV bool GridNear(const F3& o, const GridView& g) {
+    const GridReach R = grid_reach(g);
+    const float fx = __builtin_fmaxf(__builtin_fabsf(o.x - R.lo[0]), __builtin_fabsf(o.x - R.hi[0]));
+    const float fy = __builtin_fmaxf(__builtin_fabsf(o.y - R.lo[1]), __builtin_fabsf(o.y - R.hi[1]));
+    const float fz = __builtin_fmaxf(__builtin_fabsf(o.z - R.lo[2]), __builtin_fabsf(o.z - R.hi[2]));
+    return fx * fx + fy * fy + fz * fz <= R.f2near;
+}
+
+// The query as a scan of every sphere, through the walk's own loop: the cell-ordered list as
+// one range, which holds every walked sphere at least once (the first-tested ones were tested
+// already; a sphere tested twice, or a shadow query's light against its own bar, changes
+// nothing), ended by the walk's NaN exit (plane times NaN); cx = -2 marks it, so that its end
+// is final. The loop itself is unchanged (r4_x: a scan there, with its pointer and index
+// selects, cost ~20 scalar instructions and a vmcnt(0) wait per iteration).
+LRT_DEV void GridScan(GridQuery& q, const GridView& g, GridStats* st) {
+    if (st) st->fallback += 1;
+    q.j = 0;
+    q.jend = g.cells_refs;
+    q.tnx = q.tny = q.tnz = __builtin_nanf("");
+    q.cx = -2;
+    q.mode = 0;
+}
+// The end of q's walk (mode 2): is its answer certain? Not when the origin is away from the
+// spheres and its candidates could lie beyond tsafe (q.far, GridStart) and nothing closer than
+// tsafe answered: then the query goes on as the scan (returns true).
+LRT_DEV bool GridFinish(GridQuery& q, const GridView& g, GridStats* st) {
+    if (!(q.far & (q.cx != -2)) || q.bestT < grid_reach(g).tsafe) return false;
+    GridScan(q, g, st);
+    return true;
 }
 
 // Starts q's walk along q.d (q.bestT / q.best / q.li set by the caller): the big spheres,
@@ -158,24 +195,23 @@ LRT_DEV void GridStart(GridQuery& q, const GridView& g, GridStats* st = nullptr)
     for (int k = 0; k < g.nbig; ++k) GridTest(q, g.bsph[k], g.bid[k], (q.best != -2) | (g.bid[k] != q.li));
     q.inv = f3(rcp_rn(q.d.x), rcp_rn(q.d.y), rcp_rn(q.d.z));
     q.mode = 2;
-    q.farT = __builtin_inff();
+    q.cx = 0;   // (not the scan's mark, GridScan)
+    q.far = false;
     if (g.count == 0 || g.nx == 0) return;
     // Exactness needs the DDA's rounding (2^-18 (max|o| + tEnter + ext) <= 2^-16 (max|o| + ext);
     // tEnter is at most sqrt(3) (max|o| + ext)) plus how far off its sphere the reference's own
     // hit point can be (hit_excursion, growing with |c - o|) to stay inside the padding: true for
-    // every candidate when |o| is within the near reach (o2near), for those up to a distance
-    // when it is within o2dda (GridFarT), for none beyond: a huge origin, NaN or inf scans every
-    // sphere (GridFinish, farT = -inf). Decided before the box test: its rounding grows with |o|.
-    const float fx = __builtin_fmaxf(__builtin_fabsf(q.o.x - g.clox), __builtin_fabsf(q.o.x - g.chix));
-    const float fy = __builtin_fmaxf(__builtin_fabsf(q.o.y - g.cloy), __builtin_fabsf(q.o.y - g.chiy));
-    const float fz = __builtin_fmaxf(__builtin_fabsf(q.o.z - g.cloz), __builtin_fabsf(q.o.z - g.chiz));
-    if (!(fx * fx + fy * fy + fz * fz <= g.f2near)) {   // (rare: origins away from the spheres)
-        const float o2 = dot(q.o, q.o);
-        if (!(o2 <= g.o2dda)) {
-            q.farT = -__builtin_inff();
+    // every candidate when the origin is near the spheres (GridNear), for those up to tsafe
+    // when |o| is within o2dda (GridFinish then checks the rest), for none beyond: a huge origin,
+    // NaN or inf scans every sphere (GridFinish). Decided before the box test: its rounding
+    // grows with |o| too.
+    if (!GridNear(q.o, g)) {   // (rare: origins away from the spheres)
+        const GridReach R = grid_reach(g);
+        if (!(dot(q.o, q.o) <= R.o2dda)) {   // too far for the DDA (or NaN, inf): the scan at once
+            GridScan(q, g, st);
             return;
         }
-        q.farT = GridFarT(q, g, o2);
+        q.far = !GridFarClear(q, g, R);   // decided here, where the walk's state is not live yet
     }
     const float hix = GridPlane(g.lox, g.nx, g.hx), hiy = GridPlane(g.loy, g.ny, g.hy),
                 hiz = GridPlane(g.loz, g.nz, g.hz);
@@ -268,21 +304,6 @@ LRT_DEV void GridIter(GridQuery& q, const GridView& g, GridStats* st) {
     }
 }
 
-// The end of q's query: the scan of every sphere when the walk's answer is not certain
-// (GridFarT, or a huge origin): the reference's own scan over the whole scene in index order
-// (the spheres tested already again: an equal (cand, id) changes nothing, and a shadow query's
-// light is no win over its own bar). Out of the walk's loop (the walk keeps its pointer and
-// index selects out: ~20 scalar instructions and a vmcnt(0) wait per iteration, r4_x).
-LRT_DEV void GridFinish(GridQuery& q, const GridView& g, GridStats* st) {
-    if (!(q.bestT < q.farT)) {
-        if (st) {
-            st->fallback += 1;
-            st->spheres += g.count;
-        }
-        for (int k = 0; k < g.count; ++k) GridTest(q, g.all[k], k);
-    }
-}
-
 LRT_DEV int ClosestHitGrid(const F3& o, const F3& d, const GridView& g, float& tOut, GridStats* st = nullptr) {
     GridQuery q;
     q.o = o;
@@ -291,8 +312,9 @@ LRT_DEV int ClosestHitGrid(const F3& o, const F3& d, const GridView& g, float& t
     q.best = -1;
     q.li = -1;
     GridStart(q, g, st);
-    while (q.mode != 2) GridIter(q, g, st);
-    GridFinish(q, g, st);
+    do {
+        while (q.mode != 2) GridIter(q, g, st);
+    } while (GridFinish(q, g, st));
     tOut = q.bestT;
     return q.best;
 }
@@ -310,8 +332,9 @@ LRT_DEV bool ShadowReachesLightGrid(const F3& o, const F3& d, int li, const floa
     q.best = -2;
     q.li = li;
     GridStart(q, g, st);
-    while ((q.mode != 2) & (q.best == -2)) GridIter(q, g, st);
-    if (q.best == -2) GridFinish(q, g, st);   // (a sphere that beat the light is an answer already)
+    do {   // (a sphere that beat the light is an answer already)
+        while ((q.mode != 2) & (q.best == -2)) GridIter(q, g, st);
+    } while ((q.best == -2) && GridFinish(q, g, st));
     return q.best == -2;
 }
 
@@ -336,8 +359,7 @@ template <int kL = 0>
 LRT_DEV void GridDualStep(GridQuery& q, const GridView& g, GridStats* st) {
     GridIter<kL>(q, g, st);
     const bool qdone = (q.mode == 2) | (q.sh & (q.best != -2));
-    if (qdone) {
-        if (!q.sh | (q.best == -2)) GridFinish(q, g, st);
+    if (qdone && !((!q.sh | (q.best == -2)) && GridFinish(q, g, st))) {
         if (q.sh) {
             q.lit = q.best == -2;   // nothing beat the light
             q.sh = false;

@@ -74,8 +74,7 @@ struct GridHost {
     // exactness reach (GridView): the walk alone is exact for |o| <= reach_near; up to a
     // distance (GridFarT) for |o| <= reach_dda
     double reach_near = 0, reach_dda = 0;
-    float clo[3] = {0, 0, 0}, chi[3] = {0, 0, 0};   // the walked spheres' centre box
-    float f2near = 0, o2dda = 0, tsafe = 0, conea = 0, coneb = 0;
+    GridReach R = {};
     int count = 0;
     // build statistics (the policy)
     double mean_refs = 0;   // references per non-empty cell
@@ -86,10 +85,7 @@ struct GridHost {
 // sphere of the box (more cells: fewer spheres per cell, more cell steps per ray).
 // The pad serves candidates up to kGridSafe scene radii from the origin (and the DDA origins
 // up to kGridDda), see the Padding note below.
-#ifndef LRT_GRID_SAFE
-#define LRT_GRID_SAFE 1.6
-#endif
-constexpr double kGridSafe = LRT_GRID_SAFE;
+constexpr double kGridSafe = 1.6;
 constexpr double kGridDda = 8.0;
 
 inline void build_grid_at(const lrt_sphere* s, int n, const std::vector<float4>& sph, float density, GridHost& G) {
@@ -234,17 +230,22 @@ inline void build_grid_at(const lrt_sphere* s, int n, const std::vector<float4>&
     G.ext = 0.0f;
     for (int k = 0; k < 3; ++k) G.ext = std::max(G.ext, std::max(std::fabs(lo[k]), std::fabs(hi[k])));
     G.pad = pad0;
-    // near: |c - o| + r <= (the farthest corner of the centre box from o) + rmax <= dsafe
-    centre_box(s, in, G.clo, G.chi);
+    // near: |c - o| + r <= (the farthest corner of the grid's box from o) + rmax <= dsafe
     G.reach_near = std::max(0.0, dsafe - rmax);   // (a distance from the farthest corner)
     G.reach_dda = std::max(reach_dda, G.reach_near + rs);
-    G.tsafe = (float)(tsafe * (1.0 - 1e-6));
-    G.f2near = reach_sq(G.reach_near);
-    G.o2dda = reach_sq(G.reach_dda);
+    G.R.tsafe = (float)(tsafe * (1.0 - 1e-6));
+    G.R.f2near = reach_sq(G.reach_near);
+    G.R.o2dda = reach_sq(G.reach_dda);
     {
         const double c1 = std::sqrt(std::ldexp(1.0, -19)) + std::ldexp(24.0, -24);   // hit_excursion(D) <= c1 D
-        G.coneb = (float)(1.004 * c1 * (1.0 + 1.0 / 1024));
-        G.conea = (float)(3.02 * rmax * c1 * (1.0 + 1.0 / 1024));
+        if (!((double)kConeB >= 1.004 * c1 * (1.0 + 1.0 / 1024))) abort();   // (lrt_grid.h's constant)
+        // plus GridFarClear's rounding: its values stay below reach_dda + ext + tsafe (+ a)
+        for (int k = 0; k < 3; ++k) {
+            G.R.lo[k] = G.lo[k];
+            G.R.hi[k] = G.lo[k] + (float)nn[k] * G.h[k];   // GridPlane(lo, n, h)
+        }
+        G.R.conea = (float)(3.02 * rmax * c1 * (1.0 + 1.0 / 1024) +
+                          std::ldexp(G.reach_dda + (double)G.ext + tsafe + 1.0, -18));
     }
     // cell lists (CSR), spheres in index order within a cell
     const long long ncells = (long long)nn[0] * nn[1] * nn[2];
@@ -316,17 +317,7 @@ inline GridView grid_view_host(const GridHost& G, const float4* all) {
     g.ihy = G.ih[1];
     g.ihz = G.ih[2];
     g.pad = G.pad;
-    g.clox = G.clo[0];
-    g.cloy = G.clo[1];
-    g.cloz = G.clo[2];
-    g.chix = G.chi[0];
-    g.chiy = G.chi[1];
-    g.chiz = G.chi[2];
-    g.f2near = G.f2near;
-    g.o2dda = G.o2dda;
-    g.tsafe = G.tsafe;
-    g.conea = G.conea;
-    g.coneb = G.coneb;
+    g.reach = &G.R;
     g.ext = G.ext;
     g.on = 1;
     g.cells_refs = (unsigned)G.rsph.size();
@@ -337,10 +328,7 @@ inline GridView grid_view_host(const GridHost& G, const float4* all) {
 // random points in the box in random directions (bounce and shadow rays) and from a shell
 // around it towards random points in it (camera rays); a sphere test counts 1, a cell step
 // kGridCellCost (its 8-byte load sits on the walk's critical path). Deterministic.
-#ifndef LRT_GRID_CELL_COST
-#define LRT_GRID_CELL_COST 1.5
-#endif
-constexpr double kGridCellCost = LRT_GRID_CELL_COST;
+constexpr double kGridCellCost = 1.5;
 inline double grid_cost(const GridHost& G, const std::vector<float4>& sph) {
     if (G.nx == 0) return 0.0;
     const GridView g = grid_view_host(G, sph.data());
@@ -396,13 +384,7 @@ inline double grid_cost(const GridHost& G, const std::vector<float4>& sph) {
 // number. On config 4's field (a jittered 36 x 28 lattice of spheres) the model picks 36 x 1 x
 // 29 cells, one lattice site each: 2.6-2.9 sphere tests per ray against 4.1-4.6 at density 2
 // (tools/accel_stats.py); measured densities 0.5-2 ran 163-185 ms (profiles/r4_e, r4_f).
-// LRT_GRID_DENSITY fixes one instead.
 inline void build_grid_host(const lrt_sphere* s, int n, const std::vector<float4>& sph, GridHost& G) {
-    if (const char* e = getenv("LRT_GRID_DENSITY")) {
-        const float v = (float)atof(e);
-        build_grid_at(s, n, sph, v > 0.05f && v < 64.0f ? v : 1.0f, G);
-        return;
-    }
     double best = 0.0;
     bool have = false;
     for (float dens : {0.5f, 0.6f, 0.75f, 0.9f, 1.0f, 1.25f, 1.5f, 2.0f, 3.0f}) {

@@ -156,8 +156,8 @@ int host_chunks(bool lookahead) {
 // (main.cpp:165,187). So a pipelined DrawTest call also renders the colours of the next
 // frame, on a stream of their own that runs beside this call's DMA and PCIe-write lerps (a
 // hit: from the call's start; a miss: after its own render), CU-masked so that the lerps
-// still find CUs (LRT_LOOKAHEAD_RESERVED, default 32 = 4 per XCD; 0-32 within 0.01 ms pinned,
-// 32 best pageable: profiles/r3_o); the call returns once its
+// still find CUs (32 = 4 per XCD; 0-32 within 0.01 ms pinned, 32 best pageable:
+// profiles/r3_o); the call returns once its
 // own work is done. A later call asking for exactly that render (desc and scene version
 // compared) lerps those colours and skips its render, so the render leaves the critical
 // path (DMA in -> lerp -> PCIe out); any other call renders as before. Same kernel, same
@@ -171,13 +171,7 @@ bool draw_lookahead_on() {
     return on;
 }
 
-int lookahead_reserved_cus() {
-    static const int k = [] {
-        const char* e = getenv("LRT_LOOKAHEAD_RESERVED");
-        return e ? atoi(e) : 32;
-    }();
-    return k;
-}
+int lookahead_reserved_cus() { return 32; }
 
 // The look-ahead's CU-masked stream and events (init_context creates them beside the context's
 // other streams, so that each has a hardware queue of its own).

@@ -40,47 +40,31 @@
 
 namespace lrt {
 
-#ifndef LRT_V0_BLOCK
-#define LRT_V0_BLOCK 64
-#endif
-// v0 workgroup: one wave by default. A wave finished early in a multi-wave block keeps
-// its slot (and the block's LDS) until the slowest wave ends; with path lengths as
-// uneven as these, single-wave blocks keep ~1 more wave resident per SIMD.
-constexpr int kBlock = LRT_V0_BLOCK;
-static_assert(kBlock == 64 || kBlock == 256, "v0 block: 1 or 4 waves");
+// v0 workgroup: one wave. A wave finished early in a multi-wave block keeps its slot (and the
+// block's LDS) until the slowest wave ends; with path lengths as uneven as these, single-wave
+// blocks keep ~1 more wave resident per SIMD.
+constexpr int kBlock = 64;
 constexpr int kBlockWavesX = kBlock == 256 ? 2 : 1;           // waves per block in x
 constexpr int kBlockWavesY = kBlock / 64 / kBlockWavesX;       // and in y
 // a wave's pixels: 64 / kSplit of them, 8 wide (kSplit <= 8) or a single row
 constexpr int WaveCols(int split) { return split <= 8 ? 8 : 64 / split; }
-#ifndef LRT_V0_DYNAMIC
-#define LRT_V0_DYNAMIC 1
-#endif
 // Work counters: same-address device-scope atomics serialise at ~12 ns each (measured
 // ~80/us chip-wide), so v0's tile queue and ray count are split over kV0Queues
 // counters, each on its own 512-B line; block b serves queue b % kV0Queues, which owns
 // tiles q, q + kV0Queues, ...
-#ifndef LRT_V0_QUEUES
-#define LRT_V0_QUEUES 16
-#endif
-constexpr int kV0Queues = LRT_V0_QUEUES;
+constexpr int kV0Queues = 16;
 constexpr int kCtrStride = 64;   // u64s between counters
-static_assert(!LRT_V0_DYNAMIC || kBlock == 64, "dynamic v0 tiles are fetched per wave: one wave per block");
 
 constexpr int kMaxDepthSupported = 64;
 
 // 4 waves per SIMD: caps VGPRs at 128. The MAXD 20/64 and BVH instances otherwise
 // take 129-144 and drop to 3 waves (config 3: 4.44 -> 4.15 ms, config 4: 587 -> 538 ms
 // with the cap; the BVH instances spill 28-40 B/lane to scratch, which costs less).
-#ifndef LRT_V0_WAVES_PER_EU
-#define LRT_V0_WAVES_PER_EU 4
-#endif
+constexpr int kWavesPerEU = 4;
 // Samples per round of a tile, at most: with pixels x frames <= kPoolSamples a tile has one
 // round. Config 4 (64 spp): 1024 (16 px) 229 ms, 2048 (32 px) 222, 4096 (64 px) 221;
 // config 5 (256 spp, one GPU): 1024 (4 px) 3876 ms, 4096 (16 px) 3602 (profiles/r2_p2).
-#ifndef LRT_POOL_SAMPLES
-#define LRT_POOL_SAMPLES 4096
-#endif
-constexpr int kPoolSamples = LRT_POOL_SAMPLES;
+constexpr int kPoolSamples = 4096;
 
 struct KernelArgs {
     CameraDev cam;
@@ -97,7 +81,7 @@ struct KernelArgs {
     BvhView bv;
     GridView gv;
     int bvh_stack_offset;   // bytes into dynamic LDS
-    int grid_lds_offset;    // pool kernel, LRT_POOL_GRID_WPB blocks: the grid's LDS copy (bytes), or 0
+    int grid_lds_offset;    // pool kernel, kPoolGridWaves blocks: the grid's LDS copy (bytes), or 0
     float4* ovf;            // recursion stack levels >= kTraceLdsLevels (null when maxDepth fits)
     unsigned long long* wtrace;   // LRT_EXP_WAVETRACE builds only: per-wave start/end/ids
     unsigned long long* tiles;    // this launch's counters: [q] tile queue, [kV0Queues + q] finished
@@ -215,6 +199,7 @@ struct Context {
     int* d_grid_rid = nullptr;
     float4* d_grid_bsph = nullptr;
     int* d_grid_bid = nullptr;
+    GridReach* d_grid_reach = nullptr;
     GridView gv{};
     bool grid_pick = false;
     bool grid_ok = false;      // any scene: the grid applies (LRT_F_GRID below kBvhMinSpheres)

@@ -24,9 +24,6 @@
 
 namespace lrt {
 
-#ifndef LRT_POOL_PACKET
-#define LRT_POOL_PACKET 0
-#endif
 enum : int { kPoolIdle = 0, kPoolTrace = 1, kPoolDone = 2, kPoolEnded = 3 };
 
 template <int kPix>
@@ -55,14 +52,11 @@ __device__ __forceinline__ KArgPtr opaque_args() { return nullptr; }
 
 // The grid's spheres tested first by every query (the ground, the light: GridStart) are read
 // from an LDS copy (at a.bvh_stack_offset: the grid has no traversal stack) instead of through
-// L1/L2, and their uniform loads leave the walk's latency chain (LRT_GRID_BIG_LDS).
-#ifndef LRT_GRID_BIG_LDS
-#define LRT_GRID_BIG_LDS 1
-#endif
+// L1/L2, and their uniform loads leave the walk's latency chain.
 template <int kAcc, int kW>
 __device__ __forceinline__ GridView pool_grid_view(float4* smem) {
     GridView g = opaque_args()->gv;
-    if (LRT_GRID_BIG_LDS) {
+    {
         float4* b = reinterpret_cast<float4*>(reinterpret_cast<char*>(smem) + opaque_args()->bvh_stack_offset);
         g.bsph = b;
         g.bid = reinterpret_cast<const int*>(b + g.nbig);
@@ -77,30 +71,19 @@ __device__ __forceinline__ GridView pool_grid_view(float4* smem) {
     return g;
 }
 
-// Blocks of kW > 1 waves (LRT_POOL_GRID_WPB, grid instances): the waves of a block share one
+// Blocks of kW > 1 waves (kPoolGridWaves, grid instances): the waves of a block share one
 // LDS copy of the grid -- the cell ranges, the cell-ordered spheres and their indices
 // (config 4: 1,044 cells and 1,742 references, 43 KB) -- so the walk's dependent loads are LDS
 // reads (~50 cycles) instead of L1/L2 hits. Each wave keeps its own recursion stack, in kLv
 // levels of LDS (the rest in the global overflow stack) so that the 16 stacks and the grid
 // fit in the CU's 160 KB.
-#ifndef LRT_POOL_GRID_WPB
-#define LRT_POOL_GRID_WPB 16
-#endif
-#ifndef LRT_POOL_GRID_LDS_LEVELS
-#define LRT_POOL_GRID_LDS_LEVELS 7
-#endif
+constexpr int kPoolGridWaves = 16;
+constexpr int kPoolGridLdsLevels = 7;
 template <int kW>
-constexpr int pool_lds_levels() { return kW > 1 ? LRT_POOL_GRID_LDS_LEVELS : kTraceLdsLevels; }
+constexpr int pool_lds_levels() { return kW > 1 ? kPoolGridLdsLevels : kTraceLdsLevels; }
 
-#ifndef LRT_POOL_OVF_ZERO
-#define LRT_POOL_OVF_ZERO 1
-#endif
-// Waves per SIMD the grid instances are compiled for (LRT_POOL_GRID_WAVES, A/B)
-#ifndef LRT_POOL_GRID_WAVES
-#define LRT_POOL_GRID_WAVES LRT_V0_WAVES_PER_EU
-#endif
 template <int MAXD, bool kLds, int kAcc, int kPix, int kNS = 0, int kW = 1>
-__global__ __launch_bounds__(64 * kW, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : LRT_V0_WAVES_PER_EU) void pool_kernel(
+__global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
     const KernelArgs a) {
     static_assert(kNS == 0 || (kLds && !kAcc), "a fixed sphere count is for the LDS linear scan");
     static_assert(kW == 1 || (kAcc == kAccGrid && !kLds), "multi-wave blocks: the grid instance");
@@ -135,7 +118,7 @@ __global__ __launch_bounds__(64 * kW, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : L
         for (int i = lane; i < 3 * a.count; i += 64) s_mat[i] = a.mats[i];
         for (int i = lane; i < a.nlights; i += 64) s_lights[i] = a.lights[i];
     }
-    if (kAcc == kAccGrid && LRT_GRID_BIG_LDS) {   // (pool_grid_view)
+    if (kAcc == kAccGrid) {   // (pool_grid_view)
         float4* b = reinterpret_cast<float4*>(reinterpret_cast<char*>(smem) + a.bvh_stack_offset);
         for (int i = tid; i < a.gv.nbig; i += 64 * kW) {
             b[i] = a.gv.bsph[i];
@@ -187,29 +170,25 @@ __global__ __launch_bounds__(64 * kW, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : L
     // material id, bit 15 set when the level's matE + lightE is exactly +0, which then needs no
     // float4 at all -- the fold adds the literal +0 the stored value was, parallel.cpp:214) and
     // the float4 only for the others. Deep levels are mostly glass and metal chains, whose
-    // events add nothing (LRT_POOL_OVF_ZERO=0: a float4 per level, round 3).
+    // events add nothing (round 3 stored a float4 per level).
     float4* const gstk = a.ovf + gtid;
     unsigned short* const gid =
         reinterpret_cast<unsigned short*>(a.ovf + gthreads * (size_t)(a.maxDepth - kLv)) + gtid;
     auto put = [&](int lvl, float4 v) {
         if (MAXD <= kLv || lvl < kLv) {
             lstk[lvl * 64] = v;
-        } else if (LRT_POOL_OVF_ZERO) {
+        } else {
             const size_t o = (size_t)(lvl - kLv) * gthreads;
             const bool z = (__float_as_uint(v.x) | __float_as_uint(v.y) | __float_as_uint(v.z)) == 0u;
             gid[o] = (unsigned short)(__float_as_int(v.w) | (z ? 0x8000 : 0));
             if (!z) gstk[o] = v;
-        } else {
-            gstk[(size_t)(lvl - kLv) * gthreads] = v;
         }
     };
     auto get = [&](int lvl) -> float4 {
         if (MAXD <= kLv || lvl < kLv) return lstk[lvl * 64];
         const size_t o = (size_t)(lvl - kLv) * gthreads;
-        if (LRT_POOL_OVF_ZERO) {
-            const unsigned t = gid[o];
-            if (t & 0x8000u) return make_float4(0.0f, 0.0f, 0.0f, __int_as_float((int)(t & 0x7fffu)));
-        }
+        const unsigned t = gid[o];
+        if (t & 0x8000u) return make_float4(0.0f, 0.0f, 0.0f, __int_as_float((int)(t & 0x7fffu)));
         return gstk[o];
     };
     // this wave's colour slots: RGB, 12 B per sample (the 4th float was never read)
@@ -309,13 +288,9 @@ __global__ __launch_bounds__(64 * kW, kAcc == kAccGrid ? LRT_POOL_GRID_WAVES : L
                     if (__ballot(state == kPoolIdle || state == kPoolEnded) == 0) break;   // the pool is dry
                     continue;
                 }
-                // LRT_POOL_PACKET: camera rays that all start together (a round's first
-                // iteration) take the packet traversal (lrt_bvh.h). Off: without the packet
-                // code the instance keeps its traversal state in fewer registers (config 4:
-                // 222.4 -> 209.8 ms/step, profiles/r2_q2)
-                const bool coherent = kAcc == kAccBvh && LRT_POOL_PACKET && LRT_PACKET_DEPTH > 0 &&
-                                      __ballot(state == kPoolTrace && depth != 0) == 0 &&
-                                      __ballot(state == kPoolTrace && pend) == 0;
+                // (no packet traversal here: without its code the instance keeps its traversal
+                // state in fewer registers, config 4: 222.4 -> 209.8 ms/step, profiles/r2_q2)
+                constexpr bool coherent = false;
                 sec_enter(sc, kSecOther, false);
                 // ---- one bounce of every traced path: Trace's body (parallel.cpp:202-226) ----
                 if (state == kPoolTrace) {

@@ -6,28 +6,23 @@
 
 namespace lrt {
 
-// Waves per block of the grid instance (LRT_POOL_GRID_WPB blocks share the grid's LDS copy);
-// 1 when the grid does not fit beside the waves' stacks, or with LRT_POOL_GRID_WPB=1 (A/B).
+// Waves per block of the grid instance (kPoolGridWaves blocks share the grid's LDS copy); 1
+// when the grid does not fit beside the waves' stacks.
 inline int pool_grid_wpb(const KernelArgs& a, size_t stack_w, size_t shared_b, size_t* grid_b) {
     const size_t ncell = (size_t)a.gv.nx * a.gv.ny * a.gv.nz, nref = a.gv.cells_refs;
     *grid_b = (16 * nref + 8 * ncell + 4 * nref + 15) / 16 * 16;
-    static int env = -1;
-    if (env < 0) {
-        const char* v = getenv("LRT_POOL_GRID_WPB");
-        env = v ? atoi(v) : LRT_POOL_GRID_WPB;
-    }
-    if (env != LRT_POOL_GRID_WPB || !a.gv.on || a.gv.nx == 0) return 1;
+    if (!a.gv.on || a.gv.nx == 0) return 1;
     int dev = 0, maxb = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&maxb, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess)
         return 1;
-    return LRT_POOL_GRID_WPB * stack_w + shared_b + *grid_b <= (size_t)maxb ? LRT_POOL_GRID_WPB : 1;
+    return kPoolGridWaves * stack_w + shared_b + *grid_b <= (size_t)maxb ? kPoolGridWaves : 1;
 }
 
 template <int MAXD, int kPix>
 int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     constexpr int TX = PoolTile<kPix>::X, TY = PoolTile<kPix>::Y;
-    constexpr int kW = LRT_POOL_GRID_WPB;
+    constexpr int kW = kPoolGridWaves;
     const long long ntiles = (long long)((xc + TX - 1) / TX) * ((rows + TY - 1) / TY);
     const int acc = a.gv.on ? kAccGrid : a.bv.on ? kAccBvh : kAccScan;
     // the BVH's traversal stack, or the grid's first-tested spheres (pool_grid_view)
@@ -82,17 +77,9 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     a.ovf = nullptr;
     a.colbuf = nullptr;
     a.tiles = ctx().d_tiles + (size_t)(ctx().tiles_next++ % kQueueSlots) * kTileSetU64;
-    {   // waiting lanes that trigger a refill (fold + next samples); LRT_POOL_REFILL_MIN.
-        // Measured (profiles/r2_p2): config 3 2.31 -> 2.05 ms/step at 16 (vs 1), config 4 and
-        // config 2 neutral
-        static int env = -1;
-        if (env < 0) {
-            const char* v = getenv("LRT_POOL_REFILL_MIN");
-            env = v ? atoi(v) : 0;
-            if (env <= 0 || env > 64) env = 16;
-        }
-        a.regenMin = env;
-    }
+    // waiting lanes that trigger a refill (fold + next samples). Measured (profiles/r2_p2):
+    // config 3 2.31 -> 2.05 ms/step at 16 (vs 1), config 4 and config 2 neutral
+    a.regenMin = 16;
     a.poolSlots = kPix * std::min(a.frames, kPoolSamples / kPix);   // one round's samples
     const size_t nwaves = (size_t)grid.x * wpb;
     e = hipMallocAsync((void**)&a.colbuf, sizeof(float) * 3 * (size_t)a.poolSlots * nwaves, s);

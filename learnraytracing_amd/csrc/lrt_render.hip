@@ -140,7 +140,7 @@ const char* acc_name(int acc) { return acc == kAccGrid ? "grid" : acc == kAccBvh
 // Pixels per pool tile: a round holds kPoolSamples samples, so more frames -> fewer pixels.
 // Bigger tiles make bigger pools (a round's tail, its last paths with most lanes idle, is a
 // smaller share) but fewer tiles per wave (the launch's tail). 64 px at most by default:
-// 128-px tiles (LRT_POOL_PIX_MAX=128; taken only while every resident wave still gets one)
+// 128-px tiles (taken only while every resident wave still gets one)
 // run config 2 pipelined over two streams at 0.2357/0.2373 ms/step against 0.2465/0.2476 and
 // config 3 at 1.942/1.936 against 1.950/1.953, but a launch alone at 0.363-0.412 ms against
 // 0.286-0.300 (config 3: 2.47-2.66 ms against 2.07-2.09): the few heavy 128-px tiles set the
@@ -151,10 +151,7 @@ int pool_tiles(int pix, int xc, int rows) {
     return ((xc + tx - 1) / tx) * ((rows + ty - 1) / ty);
 }
 int pool_pixels(int frames, int xc, int rows) {
-    static const int cap = [] {   // LRT_POOL_PIX_MAX: largest tile (A/B)
-        const char* e = getenv("LRT_POOL_PIX_MAX");
-        return e ? atoi(e) : 64;
-    }();
+    constexpr int cap = 64;   // largest tile (128 px: +4 % pipelined, +25-35 % alone, profiles/r3_ag)
     const long long slots = 16LL * ctx().num_cus;   // resident waves (4 per SIMD)
     for (int pix : {256, 128, 64, 32, 16})
         if (cap >= pix && pix * frames <= kPoolSamples && (pix <= 64 || pool_tiles(pix, xc, rows) >= slots))

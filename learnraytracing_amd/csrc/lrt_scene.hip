@@ -27,7 +27,7 @@ const lrt_material kDefaultMats[9] = {
 
 constexpr int kBvhLeaf = 6;   // leaf size (LRT_BVH_LEAF overrides, 1..16; config 4: 4 -> 350 ms, 6 -> 335, 8 -> 336)
 constexpr int kBvhMaxBuildDepth = 22;   // < kBvhStackLevels
-constexpr int kBvhSahMaxDepth = 12;     // SAH splits above this depth, median splits below (LRT_BVH_SAH_DEPTH)
+constexpr int kBvhSahMaxDepth = 12;     // SAH splits above this depth, median splits below
 
 // ---- BVH build (host): SAH splits, median splits on the longest centroid axis deeper down
 struct BvhPrim {
@@ -40,9 +40,7 @@ struct BvhBuilder {
     std::vector<int> lid;
     const std::vector<float4>* sph = nullptr;
     int max_depth = 0;   // deepest internal node (root = 0)
-    bool sah = true;     // SAH splits (LRT_BVH_SPLIT=median: median of the longest centroid axis)
     int leaf = kBvhLeaf;
-    int sahDepth = kBvhSahMaxDepth;
 
     void sort_axis(int b, int e, int k) {
         std::sort(P.begin() + b, P.begin() + e, [k](const BvhPrim& x, const BvhPrim& y) {
@@ -86,7 +84,7 @@ struct BvhBuilder {
         for (int k = 1; k < 3; ++k)
             if (ch[k] - cl[k] > ch[axis] - cl[axis]) axis = k;
         int mid = begin + n / 2;
-        if (sah && depth < sahDepth) {
+        if (depth < kBvhSahMaxDepth) {
             // surface-area heuristic over every split of the centroid order on each axis
             // (full sweep: scenes are at most a few thousand spheres); only above
             // kBvhSahMaxDepth, so the depth bound of the median split still holds
@@ -170,14 +168,7 @@ void build_bvh_host(const lrt_sphere* s, int n, const std::vector<float4>& sph, 
     std::vector<int> big;
     BvhBuilder B;
     B.sph = &sph;
-    {
-        const char* e = getenv("LRT_BVH_SPLIT");
-        B.sah = !(e && strcmp(e, "median") == 0);
-        const char* l = getenv("LRT_BVH_LEAF");
-        if (l) B.leaf = std::min(16, std::max(1, atoi(l)));
-        const char* sd = getenv("LRT_BVH_SAH_DEPTH");
-        if (sd) B.sahDepth = std::min(kBvhMaxBuildDepth, std::max(0, atoi(sd)));
-    }
+    if (const char* l = getenv("LRT_BVH_LEAF")) B.leaf = std::min(16, std::max(1, atoi(l)));   // (tests: deep trees)
     std::vector<int> tree;
     for (int i = 0; i < n; ++i) {
         const bool finite = std::isfinite(s[i].center.x) && std::isfinite(s[i].center.y) &&
@@ -315,13 +306,14 @@ void free_scene(Context& c) {
     c.bvh_on = 0;
     c.bvh_built = false;
     for (void* p : {(void*)c.d_grid_cells, (void*)c.d_grid_rsph, (void*)c.d_grid_rid, (void*)c.d_grid_bsph,
-                    (void*)c.d_grid_bid})
+                    (void*)c.d_grid_bid, (void*)c.d_grid_reach})
         if (p) (void)hipFree(p);
     c.d_grid_cells = nullptr;
     c.d_grid_rsph = nullptr;
     c.d_grid_rid = nullptr;
     c.d_grid_bsph = nullptr;
     c.d_grid_bid = nullptr;
+    c.d_grid_reach = nullptr;
     c.gv = GridView{};
     c.grid_pick = false;
     c.grid_ok = false;
@@ -387,6 +379,7 @@ static int upload_grid(Context& c, const GridHost& G) {
     LRT_HIP(upload(c.d_grid_rid, G.rid));
     LRT_HIP(upload(c.d_grid_bsph, G.bsph));
     LRT_HIP(upload(c.d_grid_bid, G.bid));
+    LRT_HIP(upload(c.d_grid_reach, std::vector<GridReach>(1, G.R)));
     GridView& g = c.gv;
     g = grid_view_host(G, c.d_sph);
     g.cells = c.d_grid_cells;
@@ -394,6 +387,7 @@ static int upload_grid(Context& c, const GridHost& G) {
     g.rid = c.d_grid_rid;
     g.bsph = c.d_grid_bsph;
     g.bid = c.d_grid_bid;
+    g.reach = c.d_grid_reach;
     c.grid_built = true;
     return LRT_OK;
 }

@@ -49,14 +49,8 @@ LRT_DEV F3 cross(F3 a, F3 b) {                                                  
 // Operands outside those ranges (or NaN) send the whole wave through the generic
 // sequence: a wave-uniform branch, essentially never taken. Host builds (the BVH
 // diagnostics) use the plain operations.
-#ifndef LRT_FAST_SQRT
-#define LRT_FAST_SQRT 1
-#endif
-#ifndef LRT_FAST_RCP
-#define LRT_FAST_RCP 1
-#endif
 LRT_DEV float sqrt_rn(float x) {
-#if LRT_FAST_SQRT && defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
     float s = __builtin_amdgcn_sqrtf(x);
     const float sd = __int_as_float(__float_as_int(s) - 1);
     const float su = __int_as_float(__float_as_int(s) + 1);
@@ -71,7 +65,7 @@ LRT_DEV float sqrt_rn(float x) {
 #endif
 }
 LRT_DEV float rcp_rn(float x) {
-#if LRT_FAST_RCP && defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
     float r = __builtin_amdgcn_rcpf(x);
     float e = __builtin_fmaf(-x, r, 1.0f);
     r = __builtin_fmaf(e, r, r);
@@ -501,13 +495,7 @@ LRT_DEV bool Scatter(const Material& mat, const Ray& r_in, const Hit& rec, F3& a
 // lstk: this lane's LDS stack (kLdsLev levels, stride lstride float4); levels beyond
 // it (only when MAXD > kLdsLev) go to this lane's slice of a global overflow stack
 // (gstk, stride gstride; L2-resident -- few paths get that deep).
-#ifndef LRT_TRACE_LDS_LEVELS
-#define LRT_TRACE_LDS_LEVELS 8
-#endif
-constexpr int kTraceLdsLevels = LRT_TRACE_LDS_LEVELS;
-#ifndef LRT_DUAL_HIT
-#define LRT_DUAL_HIT 1
-#endif
+constexpr int kTraceLdsLevels = 8;
 template <int MAXD, bool kFeat, int kLdsLev, int kNS>
 LRT_DEV F3 TraceDual(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const SceneView& sc,
                      float4* lstk, int lstride, float4* gstk, size_t gstride, int ndl, F3* feat);
@@ -518,7 +506,7 @@ LRT_DEV F3 TraceDual(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, con
 template <int MAXD, int kAcc = 0, bool kFeat = false, int kLdsLev = kTraceLdsLevels, int kNS = 0>
 LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const SceneView& sc,
                  float4* lstk, int lstride, float4* gstk, size_t gstride, int ndl = 0, F3* feat = nullptr) {
-    if constexpr (!kAcc && LRT_DUAL_HIT)
+    if constexpr (!kAcc)
         return TraceDual<MAXD, kFeat, kLdsLev, kNS>(r, maxDepth, inoutRayCount, rng, sc, lstk, lstride, gstk, gstride,
                                                ndl, feat);
     auto put = [&](int lvl, float4 v) {
@@ -537,7 +525,7 @@ LRT_DEV F3 Trace(Ray r, int maxDepth, int& inoutRayCount, uint32_t& rng, const S
         int id = 0;
         ++inoutRayCount;
         // the first rays of a wave's paths start together: packet traversal (lrt_bvh.h)
-        const bool coherent = depth < LRT_PACKET_DEPTH;
+        const bool coherent = depth < kPacketDepth;
         if (!HitWorld<kAcc, kNS>(r, kMinT, kMaxT, sc, rec, id, coherent)) {
             float t = 0.5f * (r.dir.y + 1.0f);
             leaf = ((1.0f - t) * f3(1.0f, 1.0f, 1.0f) + t * f3(0.5f, 0.7f, 1.0f)) * 0.3f;

@@ -11,10 +11,6 @@
 
 namespace lrt {
 
-#ifndef LRT_V0_GRID_MULT
-#define LRT_V0_GRID_MULT 1
-#endif
-
 // AdaptiveStdvar (fragmentShader.fs.glsl:494-497) per channel, pow(x, 2) as x * x.
 LRT_DEV float adaptive_std(float lastStd, float lastMean, int n, float newVal, float newMean) {
     const float nf = (float)n;
@@ -53,7 +49,7 @@ LRT_DEV float4 lerp_feature(float4 m, F3 v, float lerpFac) {   // parallel.cpp:2
 // kNS > 0: compile-time sphere count (kDefaultSpheres for the reference's scene): the
 // closest-hit scans unroll fully (config 2: 0.359 -> 0.335 ms, config 3: 3.07 -> 2.84 ms).
 template <int MAXD, bool kLds, int kAcc, int kSplit, bool kFeat = false, bool kSamp = false, int kNS = 0>
-__global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(const KernelArgs a) {
+__global__ __launch_bounds__(kBlock, kWavesPerEU) void trace_kernel(const KernelArgs a) {
     static_assert(kNS == 0 || (kLds && !kAcc), "a fixed sphere count is for the LDS linear scan");
     static_assert(!kFeat || kSplit == 1, "feature launches keep a pixel's frames on one lane");
     static_assert(!(kFeat && kSamp), "sample mode has no features");
@@ -156,7 +152,7 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
                 fb[k] = (valid && a.feat[k]) ? a.feat[k][pix] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         }
         unsigned long long fetched = 0;
-        if (LRT_V0_DYNAMIC && lane == 0) fetched = atomicAdd(ctr, 1ull);
+        if (lane == 0) fetched = atomicAdd(ctr, 1ull);
         const int fbeg = kSamp ? a.frame0 + (task % rounds) * kSplit : a.frame0;
         const int fstop = kSamp ? fbeg + kSplit : fend;
         for (int f0 = fbeg; f0 < fstop; f0 += kSplit) {
@@ -224,11 +220,9 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
             for (int k = 0; k < 6; ++k)
                 if (valid && a.feat[k]) a.feat[k][pix] = fb[k];
         }
-        if (LRT_V0_DYNAMIC) {
+        {
             const unsigned long long n = __shfl(fetched, 0, 64) + (unsigned long long)bq;
             i = n < (unsigned long long)nq ? (int)n : nq;
-        } else {
-            i += bq;
         }
     }
     // one ray-count atomic per block: same-address atomics serialise in one L2 channel
@@ -257,16 +251,12 @@ __global__ __launch_bounds__(kBlock, LRT_V0_WAVES_PER_EU) void trace_kernel(cons
 #endif
     if (tid == 0) {
         unsigned long long t = 0;
-#ifndef LRT_EXP_NO_RAYCOUNT
         for (int w = 0; w < kBlock / 64; ++w) t += s_rays[w];
-#endif
         block_epilogue(a.tiles, a.rays, q, bq, t);
     }
 }
 
-#ifndef LRT_MAX_SPLIT
-#define LRT_MAX_SPLIT 16
-#endif
+constexpr int kMaxSplit = 16;   // lanes per pixel at most (32 / 64: no better, 4 % slower on config 4)
 
 
 template <int MAXD, int kSplit, bool kFeat = false>
@@ -303,24 +293,19 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     // Sample mode (kSamp): several rounds per pixel and fewer than 16 tasks per resident
     // wave (a row shard of a multi-GPU frame at N x spp) -- one task per (tile, round)
     // plus a merge pass, instead of one long task per tile (shard of 8: 7,200 tiles of 2
-    // rounds on 4,096 waves). LRT_SAMPLE_MODE=0 turns it off, 2 forces it (A/B, tests).
+    // rounds on 4,096 waves).
     const int rounds = (a.frames + kSplit - 1) / kSplit;
     const size_t npix = (size_t)xc * rows;
     bool samp = false;
     if constexpr (!kFeat && kSplit == 1) samp = a.sampOnly && lds && acc == kAccScan;
     if constexpr (!kFeat && kSplit >= 4) {
-        static int mode = -1;
-        if (mode < 0) {
-            const char* v = getenv("LRT_SAMPLE_MODE");
-            mode = v ? atoi(v) : 1;
-        }
         const long long slots = (long long)per_cu * cus;
-        samp = mode > 0 && lds && acc == kAccScan && rounds >= 2 && npix * (size_t)a.frames * sizeof(float4) <= (2ull << 30) &&
-               (mode == 2 || ntiles < 16 * slots);
+        samp = lds && acc == kAccScan && rounds >= 2 && npix * (size_t)a.frames * sizeof(float4) <= (2ull << 30) &&
+               ntiles < 16 * slots;
     }
     if (a.sampOnly && !samp) return fail(LRT_E_INVALID, "colours-only render: needs the LDS linear scan, one frame lane");
     const long long tasks = samp ? ntiles * rounds : ntiles;
-    long long blocks = (long long)per_cu * cus * LRT_V0_GRID_MULT;
+    long long blocks = (long long)per_cu * cus;
     // block b serves queue b % kV0Queues: every queue that owns a task needs a block, even
     // on a CU-masked stream left with fewer slots than queues (those blocks start later)
     blocks = std::max(blocks, (long long)kV0Queues);
@@ -407,21 +392,21 @@ template <int MAXD>
 int launch_split(const KernelArgs& a, bool lds, int xc, int rows, int frames, bool feat, hipStream_t s) {
     if (feat) return launch_depth<MAXD, 1, true>(a, lds, xc, rows, s);
     // one lane per frame of a pixel: the largest power of two <= frames, up to
-    // LRT_MAX_SPLIT lanes per pixel. Fewer lanes per pixel than frames means several
+    // kMaxSplit lanes per pixel. Fewer lanes per pixel than frames means several
     // rounds per wave task, i.e. fewer, longer tasks: with few pixels (one GPU's row shard
     // at 8 GPUs: 115,200 pixels at 32 spp) 7,200 tasks of 8 rounds on 4,096 waves left a
     // 1.7x tail (0.635 ms vs 0.365 for the same rays). Each lane replays its group's lerp
     // chain, so the merge costs kSplit steps per round: 16 measured best (shard of 8:
     // 0.437 ms, 32 lanes: 0.446; config 4 at 64 spp: 457 ms, 64 lanes: 478).
     int split = 1;
-    while (split * 2 <= frames && split * 2 <= LRT_MAX_SPLIT) split *= 2;
+    while (split * 2 <= frames && split * 2 <= kMaxSplit) split *= 2;
     switch (split) {
-        case 64: return launch_depth<MAXD, (LRT_MAX_SPLIT >= 64 ? 64 : 1)>(a, lds, xc, rows, s);
-        case 32: return launch_depth<MAXD, (LRT_MAX_SPLIT >= 32 ? 32 : 1)>(a, lds, xc, rows, s);
-        case 16: return launch_depth<MAXD, (LRT_MAX_SPLIT >= 16 ? 16 : 1)>(a, lds, xc, rows, s);
-        case 8: return launch_depth<MAXD, (LRT_MAX_SPLIT >= 8 ? 8 : 1)>(a, lds, xc, rows, s);
-        case 4: return launch_depth<MAXD, (LRT_MAX_SPLIT >= 4 ? 4 : 1)>(a, lds, xc, rows, s);
-        case 2: return launch_depth<MAXD, (LRT_MAX_SPLIT >= 2 ? 2 : 1)>(a, lds, xc, rows, s);
+        case 64: return launch_depth<MAXD, (kMaxSplit >= 64 ? 64 : 1)>(a, lds, xc, rows, s);
+        case 32: return launch_depth<MAXD, (kMaxSplit >= 32 ? 32 : 1)>(a, lds, xc, rows, s);
+        case 16: return launch_depth<MAXD, (kMaxSplit >= 16 ? 16 : 1)>(a, lds, xc, rows, s);
+        case 8: return launch_depth<MAXD, (kMaxSplit >= 8 ? 8 : 1)>(a, lds, xc, rows, s);
+        case 4: return launch_depth<MAXD, (kMaxSplit >= 4 ? 4 : 1)>(a, lds, xc, rows, s);
+        case 2: return launch_depth<MAXD, (kMaxSplit >= 2 ? 2 : 1)>(a, lds, xc, rows, s);
         default: return launch_depth<MAXD, 1>(a, lds, xc, rows, s);
     }
 }

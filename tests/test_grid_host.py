@@ -119,7 +119,8 @@ def test_grazing_and_surface_rays():
 
 def test_far_origins_take_the_fallback_scan():
     """Origins far beyond the scene (the walk's rounding bound exceeds the padding) scan every
-    sphere; nearer ones walk. Both exact."""
+    sphere; nearer ones walk, and the few whose answer could lie beyond the padding's reach
+    (origins away from the spheres, GridFarClear) finish with the scan. All exact."""
     g = np.random.default_rng(13)
     sph, _ = random_scene(300, 2)
     far = []
@@ -130,7 +131,7 @@ def test_far_origins_take_the_fallback_scan():
     res = gstats(sph, np.array(far, np.float32))
     assert res[3] == 0.0 and res[4] > 0.5, res
     near = gstats(sph, random_rays(g, 500, -8, 8))
-    assert near[3] == 0.0 and near[4] == 0.0, near
+    assert near[3] == 0.0 and near[4] < 0.01, near
 
 
 def test_non_finite_and_degenerate_scenes():
