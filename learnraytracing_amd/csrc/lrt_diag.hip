@@ -364,9 +364,7 @@ int lrt_accel_eval(const lrt_sphere* spheres, int count, const float* rays, int 
         g.bsph = (const float4*)up(G.bsph.data(), sizeof(float4) * G.bsph.size());
         g.bid = (const int*)up(G.bid.data(), sizeof(int) * G.bid.size());
         g.all = (const float4*)up(sph.data(), sizeof(float4) * sph.size());
-        g.reach = (const GridReach*)up(&G.R, sizeof(GridReach));
-        need.insert(need.end(), {(void*)g.cells, (void*)g.rsph, (void*)g.rid, (void*)g.bsph, (void*)g.bid, (void*)g.all,
-                                 (void*)g.reach});
+        need.insert(need.end(), {(void*)g.cells, (void*)g.rsph, (void*)g.rid, (void*)g.bsph, (void*)g.bid, (void*)g.all});
     }
     auto release = [&]() {
         for (void* p : owned) (void)hipFree(p);

@@ -30,11 +30,10 @@ namespace lrt {
 // Exactness reach (lrt_grid_build.h): an origin within sqrt(f2near) of every corner
 // of the grid's box: the walk alone is exact; otherwise, with dot(o, o) <= o2dda, the walk is
 // exact up to tsafe from o, and a ray whose candidates could lie farther (GridFarClear) scans
-// every sphere at the end unless its answer came first; beyond (or NaN): the scan. In memory,
-// not in the view: read at each use (grid_reach), the values hold no registers across the walk
-// (held in the view they added ~30 B of spills per lane to the pool kernel's grid instance).
+// every sphere at the end unless its answer came first; beyond (or NaN): the scan. (The host's
+// record; the view carries the values.)
 struct GridReach {
-    float f2near, o2dda;
+    float o2dda;
     float tsafe;   // the walk finds every candidate up to tsafe from such an origin
     float conea;   // a reference hit point at t lies within conea + kConeB t of the box (plus
                    // GridFarClear's rounding slack)
@@ -54,7 +53,8 @@ struct GridView {
     float hx, hy, hz;        // cell size per axis
     float ihx, ihy, ihz;     // 1 / cell size
     float pad;               // insertion padding (absolute)
-    const struct GridReach* reach;   // exactness reach (GridReach), read where used
+    float f2near;            // an origin this close (squared) to every corner of the box is near
+    float o2dda, tsafe, conea;   // the rest of the exactness reach (GridReach)
     float ext;               // max |coordinate| of the box
     int on;
     unsigned cells_refs;     // entries of rsph / rid (the LDS copy's size, kPoolGridWaves blocks)
@@ -90,7 +90,6 @@ struct GridQuery {
     unsigned j, jend; // the current cell's sphere range still to test
     int mode;         // 0 walking, 2 this query is over
     bool sh, lit, busy;
-    bool far;         // the walk's answer is certain only up to tsafe (GridStart, GridFinish)
 };
 
 LRT_DEV float GridPlane(float lo, int c, float h) { return lo + (float)c * h; }
@@ -116,18 +115,6 @@ LRT_DEV void GridTest(GridQuery& q, const float4& s, int id, bool on = true) {  
     q.best = w ? id : q.best;
 }
 
-LRT_DEV GridReach grid_reach(const GridView& g) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    typedef const __attribute__((address_space(4))) GridReach* P;   // (uniform: scalar loads)
-    const unsigned long long v = (unsigned long long)g.reach;
-    unsigned long long u = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(v >> 32)) << 32) |
-                           (unsigned)__builtin_amdgcn_readfirstlane((unsigned)v);
-    asm volatile("" : "+s"(u));   // loaded here, each time: not hoisted into the loop's registers
-    return *(P)u;
-#else
-    return *g.reach;
-#endif
-}
 
 // hit_excursion(D) <= c1 D (c1 = 2^-9.5 + 24 2^-24) with D <= 1.004 t + 3.02 rmax: the cone's
 // slope, 1.004 c1 (1 + 2^-10) (lrt_grid_build.h checks it)
@@ -140,50 +127,47 @@ constexpr float kConeB = 0.00139f;
 // on some axis, it is beyond the cone's slab at tsafe and moves away from it at least as fast
 // as the slab widens. No division, few registers (this runs in the pool kernel's loop, where
 // the walk's state is live: the exact cone interval, 6 reciprocals, added ~56 B of spills).
-LRT_DEV bool GridFarClear(const GridQuery& q, const GridView& g, const GridReach& R) {
-    const float a = R.conea, b = kConeB, t = R.tsafe;
+LRT_DEV bool GridFarClear(const F3& o, const F3& d, const GridView& g, float hix, float hiy, float hiz) {
+    const float a = g.conea, b = kConeB, t = g.tsafe;
     // per axis: moving away from the far side at |d| - b >= 0 and beyond it at tsafe
     auto away = [&](float o, float d, float lo, float hi) {
         const float m = d > 0.0f ? o - hi : lo - o;
         const float e = __builtin_fabsf(d) - b;
         return (e >= 0.0f) & (m - a + t * e > 0.0f);
     };
-    (void)g;
-    return away(q.o.x, q.d.x, R.lo[0], R.hi[0]) | away(q.o.y, q.d.y, R.lo[1], R.hi[1]) | away(q.o.z, q.d.z, R.lo[2], R.hi[2]);
+    return away(o.x, d.x, g.lox, hix) | away(o.y, d.y, g.loy, hiy) | away(o.z, d.z, g.loz, hiz);
 }
 
 // Is o within sqrt(f2near) of every corner of the grid's box, which holds every walked
 // sphere's centre (then every candidate's |c - o| + r stays within the distance the padding
 // serves)? False for NaN.
-LRT_DEV bool GridNear(const F3& o, const GridView& g) {
-    const GridReach R = grid_reach(g);
-    const float fx = __builtin_fmaxf(__builtin_fabsf(o.x - R.lo[0]), __builtin_fabsf(o.x - R.hi[0]));
-    const float fy = __builtin_fmaxf(__builtin_fabsf(o.y - R.lo[1]), __builtin_fabsf(o.y - R.hi[1]));
-    const float fz = __builtin_fmaxf(__builtin_fabsf(o.z - R.lo[2]), __builtin_fabsf(o.z - R.hi[2]));
-    return fx * fx + fy * fy + fz * fz <= R.f2near;
+LRT_DEV bool GridNear(const F3& o, const GridView& g, float hix, float hiy, float hiz) {
+    const float fx = __builtin_fmaxf(__builtin_fabsf(o.x - g.lox), __builtin_fabsf(o.x - hix));
+    const float fy = __builtin_fmaxf(__builtin_fabsf(o.y - g.loy), __builtin_fabsf(o.y - hiy));
+    const float fz = __builtin_fmaxf(__builtin_fabsf(o.z - g.loz), __builtin_fabsf(o.z - hiz));
+    return fx * fx + fy * fy + fz * fz <= g.f2near;
 }
 
-// The query as a scan of every sphere, through the walk's own loop: the cell-ordered list as
-// one range, which holds every walked sphere at least once (the first-tested ones were tested
-// already; a sphere tested twice, or a shadow query's light against its own bar, changes
-// nothing), ended by the walk's NaN exit (plane times NaN); cx = -2 marks it, so that its end
-// is final. The loop itself is unchanged (r4_x: a scan there, with its pointer and index
-// selects, cost ~20 scalar instructions and a vmcnt(0) wait per iteration).
-LRT_DEV void GridScan(GridQuery& q, const GridView& g, GridStats* st) {
-    if (st) st->fallback += 1;
-    q.j = 0;
-    q.jend = g.cells_refs;
-    q.tnx = q.tny = q.tnz = __builtin_nanf("");
-    q.cx = -2;
-    q.mode = 0;
+// After q's walk (mode 2): is its answer the reference's? Always when the origin is near the
+// spheres; else (the DDA's reach, o2dda, given) when the answer came before tsafe -- the walk
+// finds every candidate up to there -- or when no candidate can lie beyond tsafe (GridFarClear).
+// Decided after the walk's loop from the query's own origin and direction, so that the loop
+// carries none of it (a check and a scan in the loop cost config 4 ~10 %, profiles/r5_e).
+LRT_DEV bool GridCertain(const F3& o, const F3& d, float bestT, const GridView& g) {
+    const float hix = GridPlane(g.lox, g.nx, g.hx), hiy = GridPlane(g.loy, g.ny, g.hy),
+                hiz = GridPlane(g.loz, g.nz, g.hz);
+    if ((g.count == 0) | (g.nx == 0) || GridNear(o, g, hix, hiy, hiz)) return true;
+    return (int)(dot(o, o) <= g.o2dda) & ((int)(bestT < g.tsafe) | (int)GridFarClear(o, d, g, hix, hiy, hiz));
 }
-// The end of q's walk (mode 2): is its answer certain? Not when the origin is away from the
-// spheres and its candidates could lie beyond tsafe (q.far, GridStart) and nothing closer than
-// tsafe answered: then the query goes on as the scan (returns true).
-LRT_DEV bool GridFinish(GridQuery& q, const GridView& g, GridStats* st) {
-    if (!(q.far & (q.cx != -2)) || q.bestT < grid_reach(g).tsafe) return false;
-    GridScan(q, g, st);
-    return true;
+// The reference's own scan over the whole scene in index order, from the query's (bestT, best):
+// the spheres tested already again (an equal (cand, id) changes nothing, and a shadow query's
+// light is no win over its own bar).
+LRT_DEV void GridScanAll(GridQuery& q, const GridView& g, GridStats* st) {
+    if (st) {
+        st->fallback += 1;
+        st->spheres += g.count;
+    }
+    for (int k = 0; k < g.count; ++k) GridTest(q, g.all[k], k);
 }
 
 // Starts q's walk along q.d (q.bestT / q.best / q.li set by the caller): the big spheres,
@@ -195,26 +179,21 @@ LRT_DEV void GridStart(GridQuery& q, const GridView& g, GridStats* st = nullptr)
     for (int k = 0; k < g.nbig; ++k) GridTest(q, g.bsph[k], g.bid[k], (q.best != -2) | (g.bid[k] != q.li));
     q.inv = f3(rcp_rn(q.d.x), rcp_rn(q.d.y), rcp_rn(q.d.z));
     q.mode = 2;
-    q.cx = 0;   // (not the scan's mark, GridScan)
-    q.far = false;
     if (g.count == 0 || g.nx == 0) return;
     // Exactness needs the DDA's rounding (2^-18 (max|o| + tEnter + ext) <= 2^-16 (max|o| + ext);
     // tEnter is at most sqrt(3) (max|o| + ext)) plus how far off its sphere the reference's own
     // hit point can be (hit_excursion, growing with |c - o|) to stay inside the padding: true for
     // every candidate when the origin is near the spheres (GridNear), for those up to tsafe
-    // when |o| is within o2dda (GridFinish then checks the rest), for none beyond: a huge origin,
-    // NaN or inf scans every sphere (GridFinish). Decided before the box test: its rounding
+    // when |o| is within o2dda (GridCertain then checks the rest), for none beyond: a huge origin,
+    // NaN or inf scans every sphere (GridCertain). Decided before the box test: its rounding
     // grows with |o| too.
-    if (!GridNear(q.o, g)) {   // (rare: origins away from the spheres)
-        const GridReach R = grid_reach(g);
-        if (!(dot(q.o, q.o) <= R.o2dda)) {   // too far for the DDA (or NaN, inf): the scan at once
-            GridScan(q, g, st);
-            return;
-        }
-        q.far = !GridFarClear(q, g, R);   // decided here, where the walk's state is not live yet
-    }
     const float hix = GridPlane(g.lox, g.nx, g.hx), hiy = GridPlane(g.loy, g.ny, g.hy),
                 hiz = GridPlane(g.loz, g.nz, g.hz);
+    // near: from registers; the rest (few lanes) from memory (grid_reach: a scalar load, whose
+    // wait would also wait for the walk's LDS reads -- read at every query start it cost config
+    // 4 ~15 %)
+    // (origins too far for the DDA, NaN, inf: no walk; GridCertain sends them to the scan)
+    if ((int)!GridNear(q.o, g, hix, hiy, hiz) & (int)!(dot(q.o, q.o) <= g.o2dda)) return;
     // the box's slab interval; an axis the ray does not move along constrains through o
     float t0 = 0.0f, t1 = __builtin_inff();
     auto slab = [&](float o, float d, float inv, float lo, float hi) {   // (selects: no region per axis)
@@ -312,9 +291,8 @@ LRT_DEV int ClosestHitGrid(const F3& o, const F3& d, const GridView& g, float& t
     q.best = -1;
     q.li = -1;
     GridStart(q, g, st);
-    do {
-        while (q.mode != 2) GridIter(q, g, st);
-    } while (GridFinish(q, g, st));
+    while (q.mode != 2) GridIter(q, g, st);
+    if (!GridCertain(o, d, q.bestT, g)) GridScanAll(q, g, st);
     tOut = q.bestT;
     return q.best;
 }
@@ -331,10 +309,17 @@ LRT_DEV bool ShadowReachesLightGrid(const F3& o, const F3& d, int li, const floa
     q.bestT = candL;
     q.best = -2;
     q.li = li;
+    // the bar is candL from the start (only the walk's own finds lower it), so whether the walk's
+    // answer will be certain is known before it: if not, the scan instead. (GridCertain without
+    // its cone test: in the pool kernel this is the other lights' shadow query inside Scatter,
+    // where the cone test's registers added ~30 B of spills per lane to the whole kernel.)
+    if ((int)!GridNear(o, g, GridPlane(g.lox, g.nx, g.hx), GridPlane(g.loy, g.ny, g.hy), GridPlane(g.loz, g.nz, g.hz)) &
+        (int)!((int)(dot(o, o) <= g.o2dda) & (int)(candL < g.tsafe))) {
+        GridScanAll(q, g, st);
+        return q.best == -2;
+    }
     GridStart(q, g, st);
-    do {   // (a sphere that beat the light is an answer already)
-        while ((q.mode != 2) & (q.best == -2)) GridIter(q, g, st);
-    } while ((q.best == -2) && GridFinish(q, g, st));
+    while ((q.mode != 2) & (q.best == -2)) GridIter(q, g, st);
     return q.best == -2;
 }
 
@@ -350,6 +335,19 @@ LRT_DEV void GridDualInit(GridQuery& q, const F3& o, const F3& db, bool hasS, co
     q.busy = true;
     const float candL = hasS ? GridCand(o, ds, lightSph) : kMaxT;
     q.sh = candL < kMaxT;   // no shadow ray, or the light is not hit at all: not lit
+    // A shadow query the walk cannot answer for certain (GridCertain: its bar is candL, which
+    // only the walk's own finds could lower) is answered here by the scan, before the loop.
+    if (q.sh && !GridCertain(o, ds, candL, g)) {
+        GridQuery s;
+        s.o = o;
+        s.d = ds;
+        s.bestT = candL;
+        s.best = -2;
+        s.li = li;
+        GridScanAll(s, g, st);
+        q.lit = s.best == -2;
+        q.sh = false;
+    }
     q.d = q.sh ? ds : db;
     q.bestT = q.sh ? candL : kMaxT;
     q.best = q.sh ? -2 : -1;
@@ -359,7 +357,7 @@ template <int kL = 0>
 LRT_DEV void GridDualStep(GridQuery& q, const GridView& g, GridStats* st) {
     GridIter<kL>(q, g, st);
     const bool qdone = (q.mode == 2) | (q.sh & (q.best != -2));
-    if (qdone && !((!q.sh | (q.best == -2)) && GridFinish(q, g, st))) {
+    if (qdone) {
         if (q.sh) {
             q.lit = q.best == -2;   // nothing beat the light
             q.sh = false;
@@ -378,6 +376,8 @@ LRT_DEV int ClosestHitDualGrid(const F3& o, const F3& db, bool hasS, const F3& d
     GridQuery q;
     GridDualInit<kL>(q, o, db, hasS, ds, li, lightSph, g, st);
     while (q.busy) GridDualStep<kL>(q, g, st);
+    // after the loop (GridCertain), from the values the loop keeps anyway (q.d is the bounce's)
+    if (!GridCertain(q.o, q.d, q.bestT, g)) GridScanAll(q, g, st);
     lit = q.lit;
     tOut = q.bestT;
     return q.best;

@@ -75,6 +75,7 @@ struct GridHost {
     // distance (GridFarT) for |o| <= reach_dda
     double reach_near = 0, reach_dda = 0;
     GridReach R = {};
+    float f2near = 0;
     int count = 0;
     // build statistics (the policy)
     double mean_refs = 0;   // references per non-empty cell
@@ -203,7 +204,11 @@ inline void build_grid_at(const lrt_sphere* s, int n, const std::vector<float4>&
     // the DDA's share: 2^-16 (|o| + ext) for |o| <= reach_dda, with the box's padded extent
     // (ext grows by at most 2 pads, each far below the extent)
     const double ddapad = std::ldexp(reach_dda + 1.01 * ext + 1e-3, -16);
+#ifdef LRT_EXP_PAD_R4
+    auto pad_of = [&](double) { return (float)(1e-5 * ext + 2.5e-4 * span + 1e-6); };
+#else
     auto pad_of = [&](double r) { return (float)((hit_excursion(dsafe, r) + ddapad) * (1.0 + 1e-6)); };
+#endif
     const float pad0 = std::max((float)(1e-5 * ext + 2.5e-4 * span + 1e-6), pad_of(rmin));   // the largest
     float e3[3];
     double vol = 1.0;
@@ -234,7 +239,7 @@ inline void build_grid_at(const lrt_sphere* s, int n, const std::vector<float4>&
     G.reach_near = std::max(0.0, dsafe - rmax);   // (a distance from the farthest corner)
     G.reach_dda = std::max(reach_dda, G.reach_near + rs);
     G.R.tsafe = (float)(tsafe * (1.0 - 1e-6));
-    G.R.f2near = reach_sq(G.reach_near);
+    G.f2near = reach_sq(G.reach_near);
     G.R.o2dda = reach_sq(G.reach_dda);
     {
         const double c1 = std::sqrt(std::ldexp(1.0, -19)) + std::ldexp(24.0, -24);   // hit_excursion(D) <= c1 D
@@ -317,7 +322,10 @@ inline GridView grid_view_host(const GridHost& G, const float4* all) {
     g.ihy = G.ih[1];
     g.ihz = G.ih[2];
     g.pad = G.pad;
-    g.reach = &G.R;
+    g.f2near = G.f2near;
+    g.o2dda = G.R.o2dda;
+    g.tsafe = G.R.tsafe;
+    g.conea = G.R.conea;
     g.ext = G.ext;
     g.on = 1;
     g.cells_refs = (unsigned)G.rsph.size();

@@ -199,7 +199,6 @@ struct Context {
     int* d_grid_rid = nullptr;
     float4* d_grid_bsph = nullptr;
     int* d_grid_bid = nullptr;
-    GridReach* d_grid_reach = nullptr;
     GridView gv{};
     bool grid_pick = false;
     bool grid_ok = false;      // any scene: the grid applies (LRT_F_GRID below kBvhMinSpheres)

@@ -306,14 +306,13 @@ void free_scene(Context& c) {
     c.bvh_on = 0;
     c.bvh_built = false;
     for (void* p : {(void*)c.d_grid_cells, (void*)c.d_grid_rsph, (void*)c.d_grid_rid, (void*)c.d_grid_bsph,
-                    (void*)c.d_grid_bid, (void*)c.d_grid_reach})
+                    (void*)c.d_grid_bid})
         if (p) (void)hipFree(p);
     c.d_grid_cells = nullptr;
     c.d_grid_rsph = nullptr;
     c.d_grid_rid = nullptr;
     c.d_grid_bsph = nullptr;
     c.d_grid_bid = nullptr;
-    c.d_grid_reach = nullptr;
     c.gv = GridView{};
     c.grid_pick = false;
     c.grid_ok = false;
@@ -379,7 +378,6 @@ static int upload_grid(Context& c, const GridHost& G) {
     LRT_HIP(upload(c.d_grid_rid, G.rid));
     LRT_HIP(upload(c.d_grid_bsph, G.bsph));
     LRT_HIP(upload(c.d_grid_bid, G.bid));
-    LRT_HIP(upload(c.d_grid_reach, std::vector<GridReach>(1, G.R)));
     GridView& g = c.gv;
     g = grid_view_host(G, c.d_sph);
     g.cells = c.d_grid_cells;
@@ -387,7 +385,6 @@ static int upload_grid(Context& c, const GridHost& G) {
     g.rid = c.d_grid_rid;
     g.bsph = c.d_grid_bsph;
     g.bid = c.d_grid_bid;
-    g.reach = c.d_grid_reach;
     c.grid_built = true;
     return LRT_OK;
 }
