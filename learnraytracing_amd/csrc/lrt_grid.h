@@ -15,10 +15,13 @@
 // the box. The walk stops once the best candidate lies before the exit of the current cell:
 // every ray point up to that exit lies within the DDA's rounding error of a visited cell, a
 // sphere's hit point lies in its box, and the box was padded by more than that error -- so a
-// sphere not yet tested has cand > the exit >= best and can neither win nor tie. Rays whose
-// rounding bound (from |origin| and the box's extent) exceeds the padding's share scan every
-// sphere instead (origins more than ~8 scene sizes away). No stack: the walk's state is a
-// cell and three plane times, so the traversal holds fewer registers than the BVH's and no LDS.
+// sphere not yet tested has cand > the exit >= best and can neither win nor tie. The "hit
+// point lies in its box" needs the reference's own rounding: HitSphere's cancellation puts a
+// computed hit point up to hit_excursion(D, r) off the sphere (lrt_grid_build.h), growing with
+// the origin's distance D, so each sphere's padding covers it up to a distance the padding was
+// sized for, and rays from farther away are decided after their walk (GridCertain; DESIGN
+// §4.3). No stack: the walk's state is a cell and three plane times, so the traversal holds
+// fewer registers than the BVH's and no LDS.
 //
 // Walk and sphere tests share ONE loop (GridIter): an iteration advances to the next cell
 // when the current cell's list is used up, then tests one sphere. A wave therefore runs max

@@ -204,11 +204,7 @@ inline void build_grid_at(const lrt_sphere* s, int n, const std::vector<float4>&
     // the DDA's share: 2^-16 (|o| + ext) for |o| <= reach_dda, with the box's padded extent
     // (ext grows by at most 2 pads, each far below the extent)
     const double ddapad = std::ldexp(reach_dda + 1.01 * ext + 1e-3, -16);
-#ifdef LRT_EXP_PAD_R4
-    auto pad_of = [&](double) { return (float)(1e-5 * ext + 2.5e-4 * span + 1e-6); };
-#else
     auto pad_of = [&](double r) { return (float)((hit_excursion(dsafe, r) + ddapad) * (1.0 + 1e-6)); };
-#endif
     const float pad0 = std::max((float)(1e-5 * ext + 2.5e-4 * span + 1e-6), pad_of(rmin));   // the largest
     float e3[3];
     double vol = 1.0;

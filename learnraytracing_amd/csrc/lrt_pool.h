@@ -74,20 +74,24 @@ __device__ __forceinline__ GridView pool_grid_view(float4* smem) {
 // Blocks of kW > 1 waves (kPoolGridWaves, grid instances): the waves of a block share one
 // LDS copy of the grid -- the cell ranges, the cell-ordered spheres and their indices
 // (config 4: 1,044 cells and 1,742 references, 43 KB) -- so the walk's dependent loads are LDS
-// reads (~50 cycles) instead of L1/L2 hits. Each wave keeps its own recursion stack, in kLv
-// levels of LDS (the rest in the global overflow stack) so that the 16 stacks and the grid
-// fit in the CU's 160 KB.
+// reads (~50 cycles) instead of L1/L2 hits. Each wave keeps its own recursion stack (below).
 constexpr int kPoolGridWaves = 16;
-constexpr int kPoolGridLdsLevels = 7;
+// Every instance keeps kTraceLdsLevels (8) recursion levels per lane in LDS. The grid
+// instance's 16-wave blocks keep them PACKED -- planes of x, y and z floats and one of u16
+// material ids, 14 B a level instead of a float4's 16 -- so that 16 stacks of 8 levels take the
+// 112 KB that 7 float4 levels took and still fit beside the grid in the CU's 160 KB. (Round 4
+// had 7 float4 levels there and the eighth in the global overflow stack, whose per-lane
+// pointers also held registers.) Bytes per wave:
 template <int kW>
-constexpr int pool_lds_levels() { return kW > 1 ? kPoolGridLdsLevels : kTraceLdsLevels; }
+constexpr int pool_stack_bytes() { return 64 * kTraceLdsLevels * (kW > 1 ? 14 : 16); }
 
 template <int MAXD, bool kLds, int kAcc, int kPix, int kNS = 0, int kW = 1>
 __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
     const KernelArgs a) {
     static_assert(kNS == 0 || (kLds && !kAcc), "a fixed sphere count is for the LDS linear scan");
     static_assert(kW == 1 || (kAcc == kAccGrid && !kLds), "multi-wave blocks: the grid instance");
-    constexpr int kLv = pool_lds_levels<kW>();   // recursion stack levels in LDS
+    constexpr int kLv = kTraceLdsLevels;   // recursion stack levels in LDS
+    constexpr bool kPacked = kW > 1;        // (pool_stack_bytes)
     // LDS as trace_kernel: [recursion stack kTraceLdsLevels x 64][powf tables][renormalize
     // table unless kAcc][spheres][materials][lights][bvh stack at a.bvh_stack_offset]
     extern __shared__ float4 smem[];
@@ -98,7 +102,7 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
     const int wid = (int)blockIdx.x * kW + wave;
     const int nwaves = (int)gridDim.x * kW;
     (void)nwaves;
-    double* s_pow = reinterpret_cast<double*>(smem + kW * kLv * 64);
+    double* s_pow = reinterpret_cast<double*>(reinterpret_cast<char*>(smem) + kW * pool_stack_bytes<kW>());
     {
         const libm::PowTables g = libm::pow_tables();
         for (int i = tid; i < 16; i += 64 * kW) {
@@ -110,7 +114,8 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
     constexpr int kLutBytes = kAcc ? 0 : kRenormBytes;
     float* s_lut = kAcc ? nullptr : reinterpret_cast<float*>(s_pow + 64);
     if (!kAcc) renorm_lut_fill(s_lut, lane, 64);
-    float4* s_sph = smem + kW * kLv * 64 + (kPowTableBytes + kLutBytes) / 16;
+    float4* s_sph = reinterpret_cast<float4*>(reinterpret_cast<char*>(smem) + kW * pool_stack_bytes<kW>() +
+                                              kPowTableBytes + kLutBytes);
     float4* s_mat = s_sph + a.count;
     int* s_lights = reinterpret_cast<int*>(s_mat + 3 * a.count);
     if (kLds) {
@@ -162,11 +167,15 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
 #endif
 #ifdef LRT_EXP_WAVETRACE
     const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long wlast = 0, wtiles = 0;   // the last task's start, the task count
 #endif
     float4* const lstk = smem + wave * kLv * 64 + lane;   // this lane's recursion stack (LDS)
+    // (packed: the x plane at lane, then y, z, and the u16 ids after the three float planes)
+    float* const pstk = reinterpret_cast<float*>(reinterpret_cast<char*>(smem) + wave * pool_stack_bytes<kW>()) + lane;
+    unsigned short* const pids = reinterpret_cast<unsigned short*>(pstk - lane + 3 * kLv * 64) + lane;
     const size_t gtid = (size_t)wid * 64 + lane;
     const size_t gthreads = (size_t)nwaves * 64;
-    // Levels >= kLv (MAXD > 8, or kW > 1) in the global overflow stack: a u16 per level (the
+    // Levels >= kLv (MAXD > 8) in the global overflow stack: a u16 per level (the
     // material id, bit 15 set when the level's matE + lightE is exactly +0, which then needs no
     // float4 at all -- the fold adds the literal +0 the stored value was, parallel.cpp:214) and
     // the float4 only for the others. Deep levels are mostly glass and metal chains, whose
@@ -176,7 +185,14 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
         reinterpret_cast<unsigned short*>(a.ovf + gthreads * (size_t)(a.maxDepth - kLv)) + gtid;
     auto put = [&](int lvl, float4 v) {
         if (MAXD <= kLv || lvl < kLv) {
-            lstk[lvl * 64] = v;
+            if constexpr (kPacked) {
+                pstk[lvl * 64] = v.x;
+                pstk[(kLv + lvl) * 64] = v.y;
+                pstk[(2 * kLv + lvl) * 64] = v.z;
+                pids[lvl * 64] = (unsigned short)__float_as_int(v.w);
+            } else {
+                lstk[lvl * 64] = v;
+            }
         } else {
             const size_t o = (size_t)(lvl - kLv) * gthreads;
             const bool z = (__float_as_uint(v.x) | __float_as_uint(v.y) | __float_as_uint(v.z)) == 0u;
@@ -185,7 +201,12 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
         }
     };
     auto get = [&](int lvl) -> float4 {
-        if (MAXD <= kLv || lvl < kLv) return lstk[lvl * 64];
+        if (MAXD <= kLv || lvl < kLv) {
+            if constexpr (kPacked)
+                return make_float4(pstk[lvl * 64], pstk[(kLv + lvl) * 64], pstk[(2 * kLv + lvl) * 64],
+                                   __int_as_float((int)pids[lvl * 64]));
+            return lstk[lvl * 64];
+        }
         const size_t o = (size_t)(lvl - kLv) * gthreads;
         const unsigned t = gid[o];
         if (t & 0x8000u) return make_float4(0.0f, 0.0f, 0.0f, __int_as_float((int)(t & 0x7fffu)));
@@ -213,6 +234,10 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
         const int task = q + kV0Queues * i;
         const int tile = a.perm ? a.perm[task] : task;   // heaviest-first order (tile_order)
         const unsigned long long tt0 = a.tcost ? __builtin_amdgcn_s_memrealtime() : 0ull;
+#ifdef LRT_EXP_WAVETRACE
+        wlast = __builtin_amdgcn_s_memrealtime();
+        ++wtiles;
+#endif
         const int tx0 = (tile % tilesX) * TX, ty0 = (tile / tilesX) * TY;
         unsigned long long fetched = 0;
         if (lane == 0) fetched = atomicAdd(ctr, 1ull);   // consumed after the tile (hides its latency)
@@ -408,6 +433,8 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         }
+        // recording launch: the tile's cost = its wall time (the rays it traced ordered config 2
+        // worse: 0.300 against 0.276 ms alone, profiles/r5_p)
         if (a.tcost && lane == 0) a.tcost[tile] = (unsigned)(__builtin_amdgcn_s_memrealtime() - tt0);
         const unsigned long long n = __shfl(fetched, 0, 64) + (unsigned long long)bq;
         i = n < (unsigned long long)nq ? (int)n : nq;
@@ -426,8 +453,10 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
     if (lane == 0) {
         a.wtrace[4 * wid + 0] = wt0;
         a.wtrace[4 * wid + 1] = __builtin_amdgcn_s_memrealtime();
-        a.wtrace[4 * wid + 2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
-        a.wtrace[4 * wid + 3] = __builtin_amdgcn_s_getreg((15 << 11) | 20);   // XCC_ID
+        a.wtrace[4 * wid + 2] = (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) |   // HW_ID
+                                ((unsigned long long)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32) |  // XCC_ID
+                                (wtiles << 40);
+        a.wtrace[4 * wid + 3] = wlast;
     }
 #endif
     const unsigned long long total = wave_sum((unsigned long long)rays);

@@ -30,7 +30,7 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
                         : acc == kAccGrid ? (sizeof(float4) + sizeof(int)) * (size_t)a.gv.nbig : 0;
     size_t grid_b = 0;
     int wpb = acc == kAccGrid && !lds
-                  ? pool_grid_wpb(a, sizeof(float4) * pool_lds_levels<kW>() * 64,
+                  ? pool_grid_wpb(a, pool_stack_bytes<kW>(),
                                   kPowTableBytes + (bstk + 15) / 16 * 16, &grid_b)
                   : 1;
     if (wpb > 1) {
@@ -47,8 +47,9 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
                      : -1;
         if (!r || *r < 0) wpb = 1;
     }
-    const int lv = wpb > 1 ? pool_lds_levels<kW>() : kTraceLdsLevels;   // recursion stack levels in LDS
-    const size_t stack = sizeof(float4) * lv * 64 * wpb + kPowTableBytes + (acc ? 0 : kRenormBytes);
+    const int lv = kTraceLdsLevels;   // recursion stack levels in LDS (packed in multi-wave blocks)
+    const size_t stack = (wpb > 1 ? (size_t)pool_stack_bytes<kW>() * wpb : (size_t)pool_stack_bytes<1>()) +
+                         kPowTableBytes + (acc ? 0 : kRenormBytes);
     const size_t scene = lds ? sizeof(float4) * (4 * (size_t)a.count + (size_t)(a.nlights + 3) / 4 + 1) : 0;
     a.bvh_stack_offset = (int)(stack + scene);
     a.grid_lds_offset = wpb > 1 ? (int)(stack + (bstk + 15) / 16 * 16) : 0;

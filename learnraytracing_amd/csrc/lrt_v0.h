@@ -245,8 +245,9 @@ __global__ __launch_bounds__(kBlock, kWavesPerEU) void trace_kernel(const Kernel
         const size_t w = gtid >> 6;
         a.wtrace[4 * w + 0] = wt0;
         a.wtrace[4 * w + 1] = __builtin_amdgcn_s_memrealtime();
-        a.wtrace[4 * w + 2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);           // HW_ID
-        a.wtrace[4 * w + 3] = __builtin_amdgcn_s_getreg((15 << 11) | 20);          // XCC_ID
+        a.wtrace[4 * w + 2] = (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) |   // HW_ID
+                              ((unsigned long long)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32);   // XCC_ID
+        a.wtrace[4 * w + 3] = 0;
     }
 #endif
     if (tid == 0) {
