@@ -51,6 +51,8 @@ CONFIGS = {
     4: dict(width=3840, height=2160, spp=64, depth=8, scene="random1000"),
     5: dict(width=7680, height=4320, spp=256, depth=8, scene="random1000"),
 }
+# timed steps by default: a timed region of tens of ms (config 2: 200 x 0.22 ms)
+DEFAULT_STEPS = {2: 200, 3: 40, 4: 10, 5: 3}
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md, chip-level parameters (spec)
 BYTES_PER_PIXEL_SAMPLE = 24.0    # 12 B read + 12 B write of RGB per pixel-sample
 # VALU: 256 CUs x 4 SIMD32 x 32 lanes per clock x 2.4 GHz = 78.6 T lane-operations/s
@@ -261,7 +263,9 @@ def read_pmc(key: str):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default: per config, a timed region of tens of ms: config 2 200 steps "
+                         "-- 20 steps of 0.22 ms left launch and drain edges at ~8 %% of a 4.5-ms region)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
@@ -289,6 +293,8 @@ def main():
                     help="auto: the library's policy; v0: frame lanes; wf: wavefront; "
                          "pool: sample-pool regeneration (A/B)")
     args = ap.parse_args()
+    if args.steps is None:
+        args.steps = DEFAULT_STEPS.get(args.config, 20)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))

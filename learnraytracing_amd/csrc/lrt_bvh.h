@@ -327,18 +327,19 @@ LRT_DEV bool ShadowReachesLightBVH4(const F3& o, const F3& d, int li, const floa
 }
 
 
-// Two queries from one origin in ONE traversal loop (the pool kernel's bounce step,
-// lrt_pool.h): first the deferred shadow ray of the last scatter's last light (ds, light
-// li, when hasS), then the next bounce ray's closest hit (db). A lane without a shadow ray
-// starts on its bounce ray at once, so a wave runs max over lanes of (shadow + bounce)
-// node iterations instead of max(shadow) + max(bounce) in two separate loops.
+// Two queries from one origin (the pool kernel's bounce step, lrt_pool.h): first the
+// deferred shadow ray of the last scatter's last light (ds, light li, when hasS), then the
+// next bounce ray's closest hit (db). Until round 5 they shared ONE loop (a wave ran max over
+// lanes of shadow + bounce visits), but each lane's handover then came at its own visit and
+// restarted its query divergently; now every shadow query runs first and the handover is
+// taken by all those lanes together (ClosestHitDualBVH4).
 // The shadow query is the closest-hit query with its bound preset to the light's own
 // candidate, (candL, li): a sphere that would replace it is exactly one that beats the
 // light, `HitWorld(shadow ray) && hitID == li` is false (parallel.cpp:122-123), and the
 // query ends there. Same per-sphere arithmetic, conservative culling and (cand, index)
 // order as ClosestHitBVH4 / ShadowReachesLightBVH4, so both answers are bit-identical.
 // The traversal is explicit per-lane state (TravQuery) advanced one node visit at a time
-// (TravStep). Shading the lanes whose queries had ended while the others' traversals
+// (TravVisit). Shading the lanes whose queries had ended while the others' traversals
 // went on (pool-kernel variants) was measured twice and dropped (profiles/r2_p2): with the
 // queries in registers across the shading code 82 VGPRs spilled (config 4: 404-829 ms
 // instead of 226); with the queries saved to memory between a traversal phase and a
@@ -356,7 +357,6 @@ struct TravQuery {
     int sp, cur, msk;   // traversal stack depth, node, children still to visit (0: query over)
     bool sh;            // on the shadow query
     bool lit;           // the shadow query's answer, once it is over
-    bool busy;          // a query is in progress
 };
 
 LRT_DEV void TravTest(TravQuery& q, const BvhView& bv, int pos, const float4& s) {
@@ -394,7 +394,6 @@ LRT_DEV void TravInit(TravQuery& q, const F3& o, const F3& db, bool hasS, const 
     q.db = db;
     q.li = li;
     q.lit = false;
-    q.busy = true;
     const float candL = hasS ? SphereCand(o, ds, lightSph) : kMaxT;
     if (!(candL < kMaxT)) {   // no shadow ray, or the light is not hit at all: not lit
         TravStartBounce(q, bv);
@@ -411,82 +410,71 @@ LRT_DEV void TravInit(TravQuery& q, const F3& o, const F3& db, bool hasS, const 
     q.msk = bv.nnodes == 0 ? 0 : 0xF;
 }
 
-// One node visit of the lane's current query; at a query's end the shadow query hands over
-// to the bounce query, and the bounce query clears `busy`.
-LRT_DEV void TravStep(TravQuery& q, const BvhView& bv, unsigned short* stk, int stride, BvhStats* st = nullptr) {
-    bool qdone = q.msk == 0 || (q.sh && q.best != -2);   // stack exhausted, or the light is beaten
-    if (!qdone) {
-        const float mb = bv.margin + q.sr.mo + 1e-5f * q.bestT;
-        const float mbase = bv.margin + q.sr.mo;
-        int next = -1, rem = 0, nextRef = 0;
-        float nearT = __builtin_inff();
-        uint32_t lmask = 0, lpack0 = 0, lpack1 = 0;   // the node's leaves this lane hit
+// Is the lane's current query over (its stack exhausted, or the light beaten)?
+LRT_DEV bool TravOver(const TravQuery& q) { return (q.msk == 0) | (q.sh & (q.best != -2)); }
+// One node visit of the lane's current query (not over).
+LRT_DEV void TravVisit(TravQuery& q, const BvhView& bv, unsigned short* stk, int stride, BvhStats* st = nullptr) {
+    const float mb = bv.margin + q.sr.mo + 1e-5f * q.bestT;
+    const float mbase = bv.margin + q.sr.mo;
+    int next = -1, rem = 0, nextRef = 0;
+    float nearT = __builtin_inff();
+    uint32_t lmask = 0, lpack0 = 0, lpack1 = 0;   // the node's leaves this lane hit
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            if (!((q.msk >> c) & 1)) continue;
-            const float4 lo = bv.nodes[8 * q.cur + 2 * c], hi = bv.nodes[8 * q.cur + 2 * c + 1];
-            const int cnt = lrt::libm::f2u_i(hi.w);
-            if (cnt < 0) continue;
-            float tn, tf;
-            SlabTest4(lo, hi, q.o, q.sr, tn, tf);
-            const float m = __builtin_fmaf(1e-5f, __builtin_fabsf(tf), mbase);   // a margin
-            const float tfm = tf + m;   // (tn <= tf + m, tn <= bestT + mb, tf + m >= kMinT)
-            if (!(tn <= __builtin_fminf(tfm, q.bestT + mb) && tfm >= kMinT)) continue;
-            if (cnt > 0) {
-                const int ref = lrt::libm::f2u_i(lo.w);
-                // leaf position (12 bits) and count - 1 (4 bits)
-                const uint32_t e = (uint32_t)ref | ((uint32_t)(cnt - 1) << 12);
-                if (c < 2) lpack0 |= e << (16 * c);
-                else lpack1 |= e << (16 * (c - 2));
-                lmask |= 1u << c;
-            } else {
-                rem |= 1 << c;
-                if (tn < nearT) {
-                    nearT = tn;
-                    next = c;
-                    nextRef = lrt::libm::f2u_i(lo.w);
-                }
-            }
-        }
-        {   // one loop over the spheres of every leaf this lane hit
-            int cs = lmask ? __builtin_ctz(lmask) : 0, jj = 0;
-            while (lmask) {
-                const uint32_t e = ((cs < 2 ? lpack0 >> (16 * cs) : lpack1 >> (16 * (cs - 2)))) & 0xFFFFu;
-                const int pos = (int)(e & 4095u) + jj;
-                TravTest(q, bv, pos, bv.lsph[pos]);
-                if (++jj > (int)(e >> 12)) {
-                    lmask &= lmask - 1;
-                    jj = 0;
-                    cs = lmask ? __builtin_ctz(lmask) : 0;
-                }
-            }
-        }
-        if (next >= 0) {
-            rem &= ~(1 << next);
-            if (rem) StackPush(stk, stride, q.sp, q.cur, rem, st);
-            q.cur = nextRef;
-            q.msk = 0xF;
-        } else if (q.sp == 0) {
-            q.msk = 0;   // this query's traversal is complete
-        } else {   // popped children descend without a second box test (as ClosestHitBVH4)
-            --q.sp;
-            const int e = stk[q.sp * stride];
-            int cur = e >> 4, msk = e & 0xF;
-            const int c = __builtin_ctz(msk);
-            msk &= msk - 1;
-            if (msk) StackPush(stk, stride, q.sp, cur, msk, st);
-            q.cur = lrt::libm::f2u_i(bv.nodes[8 * cur + 2 * c].w);
-            q.msk = 0xF;
-        }
-        qdone = q.msk == 0 || (q.sh && q.best != -2);
-    }
-    if (qdone) {
-        if (q.sh) {
-            q.lit = q.best == -2;   // nothing beat the light
-            TravStartBounce(q, bv);
+    for (int c = 0; c < 4; ++c) {
+        if (!((q.msk >> c) & 1)) continue;
+        const float4 lo = bv.nodes[8 * q.cur + 2 * c], hi = bv.nodes[8 * q.cur + 2 * c + 1];
+        const int cnt = lrt::libm::f2u_i(hi.w);
+        if (cnt < 0) continue;
+        float tn, tf;
+        SlabTest4(lo, hi, q.o, q.sr, tn, tf);
+        const float m = __builtin_fmaf(1e-5f, __builtin_fabsf(tf), mbase);   // a margin
+        const float tfm = tf + m;   // (tn <= tf + m, tn <= bestT + mb, tf + m >= kMinT)
+        if (!(tn <= __builtin_fminf(tfm, q.bestT + mb) && tfm >= kMinT)) continue;
+        if (cnt > 0) {
+            const int ref = lrt::libm::f2u_i(lo.w);
+            // leaf position (12 bits) and count - 1 (4 bits)
+            const uint32_t e = (uint32_t)ref | ((uint32_t)(cnt - 1) << 12);
+            if (c < 2) lpack0 |= e << (16 * c);
+            else lpack1 |= e << (16 * (c - 2));
+            lmask |= 1u << c;
         } else {
-            q.busy = false;
+            rem |= 1 << c;
+            if (tn < nearT) {
+                nearT = tn;
+                next = c;
+                nextRef = lrt::libm::f2u_i(lo.w);
+            }
         }
+    }
+    {   // one loop over the spheres of every leaf this lane hit
+        int cs = lmask ? __builtin_ctz(lmask) : 0, jj = 0;
+        while (lmask) {
+            const uint32_t e = ((cs < 2 ? lpack0 >> (16 * cs) : lpack1 >> (16 * (cs - 2)))) & 0xFFFFu;
+            const int pos = (int)(e & 4095u) + jj;
+            TravTest(q, bv, pos, bv.lsph[pos]);
+            if (++jj > (int)(e >> 12)) {
+                lmask &= lmask - 1;
+                jj = 0;
+                cs = lmask ? __builtin_ctz(lmask) : 0;
+            }
+        }
+    }
+    if (next >= 0) {
+        rem &= ~(1 << next);
+        if (rem) StackPush(stk, stride, q.sp, q.cur, rem, st);
+        q.cur = nextRef;
+        q.msk = 0xF;
+    } else if (q.sp == 0) {
+        q.msk = 0;   // this query's traversal is complete
+    } else {   // popped children descend without a second box test (as ClosestHitBVH4)
+        --q.sp;
+        const int e = stk[q.sp * stride];
+        int cur = e >> 4, msk = e & 0xF;
+        const int c = __builtin_ctz(msk);
+        msk &= msk - 1;
+        if (msk) StackPush(stk, stride, q.sp, cur, msk, st);
+        q.cur = lrt::libm::f2u_i(bv.nodes[8 * cur + 2 * c].w);
+        q.msk = 0xF;
     }
 }
 
@@ -500,7 +488,16 @@ LRT_DEV int ClosestHitDualBVH4(const F3& o, const F3& db, bool hasS, const F3& d
                                BvhStats* st = nullptr) {
     TravQuery q;
     TravInit(q, o, db, hasS, ds, li, lightSph, bv);
-    while (q.busy) TravStep(q, bv, stk, stride, st);
+    // Every shadow query first, then the lanes that had one start their bounce query together,
+    // then every bounce query: each lane's handover at its own node visit ran TravStartBounce
+    // (the big spheres, the slab ray) divergently on almost every visit (as the grid's dual
+    // walk, lrt_grid.h ClosestHitDualGrid). Same queries, same order per lane: same bits.
+    if (q.sh) {
+        while (!TravOver(q)) TravVisit(q, bv, stk, stride, st);
+        q.lit = q.best == -2;   // nothing beat the light
+        TravStartBounce(q, bv);
+    }
+    while (q.msk != 0) TravVisit(q, bv, stk, stride, st);
     lit = q.lit;
     return TravResult(q, bv, tOut);
 }

@@ -92,7 +92,7 @@ struct GridQuery {
     int cx, cy, cz;   // current cell
     unsigned j, jend; // the current cell's sphere range still to test
     int mode;         // 0 walking, 2 this query is over
-    bool sh, lit, busy;
+    bool sh, lit;
 };
 
 LRT_DEV float GridPlane(float lo, int c, float h) { return lo + (float)c * h; }
@@ -335,7 +335,6 @@ LRT_DEV void GridDualInit(GridQuery& q, const F3& o, const F3& db, bool hasS, co
     q.db = db;
     q.li = li;
     q.lit = false;
-    q.busy = true;
     const float candL = hasS ? GridCand(o, ds, lightSph) : kMaxT;
     q.sh = candL < kMaxT;   // no shadow ray, or the light is not hit at all: not lit
     // A shadow query the walk cannot answer for certain (GridCertain: its bar is candL, which
@@ -357,28 +356,28 @@ LRT_DEV void GridDualInit(GridQuery& q, const F3& o, const F3& db, bool hasS, co
     GridStart<kL>(q, g, st);
 }
 template <int kL = 0>
-LRT_DEV void GridDualStep(GridQuery& q, const GridView& g, GridStats* st) {
-    GridIter<kL>(q, g, st);
-    const bool qdone = (q.mode == 2) | (q.sh & (q.best != -2));
-    if (qdone) {
-        if (q.sh) {
-            q.lit = q.best == -2;   // nothing beat the light
-            q.sh = false;
-            q.d = q.db;
-            q.bestT = kMaxT;
-            q.best = -1;
-            GridStart<kL>(q, g, st);
-        } else {
-            q.busy = false;
-        }
-    }
-}
-template <int kL = 0>
 LRT_DEV int ClosestHitDualGrid(const F3& o, const F3& db, bool hasS, const F3& ds, int li, const float4& lightSph,
                                const GridView& g, float& tOut, bool& lit, GridStats* st = nullptr) {
     GridQuery q;
     GridDualInit<kL>(q, o, db, hasS, ds, li, lightSph, g, st);
-    while (q.busy) GridDualStep<kL>(q, g, st);
+    // Every shadow walk first (to its end: the light reached, or a sphere before it), then the
+    // lanes that had one start their bounce walk TOGETHER, then every bounce walk. Round 4 ran
+    // both in one loop -- a wave took max over lanes of (shadow + bounce) iterations instead of
+    // max(shadow) + max(bounce) -- but each lane's switch from its shadow to its bounce query came
+    // at its own iteration, so GridStart (the big spheres, the slab test, the entry cell: the
+    // longest block of the walk) ran divergently on almost every iteration. Config 4: 112.7-113.2
+    // -> 83.7-83.9 ms/step (profiles/r5_r). The same queries in the same order per lane: the bits
+    // are unchanged.
+    if (q.sh) {
+        while ((q.mode != 2) & (q.best == -2)) GridIter<kL>(q, g, st);
+        q.lit = q.best == -2;   // nothing beat the light
+        q.sh = false;
+        q.d = q.db;
+        q.bestT = kMaxT;
+        q.best = -1;
+        GridStart<kL>(q, g, st);
+    }
+    while (q.mode != 2) GridIter<kL>(q, g, st);
     // after the loop (GridCertain), from the values the loop keeps anyway (q.d is the bounce's)
     if (!GridCertain(q.o, q.d, q.bestT, g)) GridScanAll(q, g, st);
     lit = q.lit;

@@ -168,12 +168,25 @@ struct Context {
         void* d_tmp = nullptr;
         size_t tmp_bytes = 0;
         hipEvent_t ev_rec = nullptr;   // after the recording launch and the sort behind it
+        bool rec_done = false;         // ev_rec seen complete: later launches need not wait on it
         int donor = -1;                // the entry whose order the recording launch borrowed
         // the streams whose launches read d_perm / wrote d_cost, each with an event after its
         // last such launch: the entry is reused only once all of them have passed it
         std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
         unsigned long long tick = 0;   // least recently used goes first
     };
+    // Per-stream scratch of the pool kernel (colour slots, overflow stack), kept from launch to
+    // launch: an allocation and a free around every launch put two more commands between
+    // consecutive kernels of a stream (profiles/r5_s). Reuse on the same stream is ordered by the
+    // stream itself; a buffer grows by a stream-ordered free + allocation on that stream.
+    struct Scratch {
+        hipStream_t s = nullptr;
+        void* p = nullptr;
+        size_t bytes = 0;
+        unsigned long long tick = 0;
+    };
+    static constexpr int kScratchSlots = 8;
+    Scratch scratch[kScratchSlots];
     static constexpr int kOrderSlots = 8;
     TileOrder order[kOrderSlots];
     unsigned long long order_tick = 0;
@@ -328,6 +341,8 @@ int camera_default(int w, int h, lrt_camera* out);
 
 // ---- lrt_render.hip
 int validate(const lrt_render_desc* d);
+// At least `bytes` of device scratch for launches on stream s (Context::scratch).
+hipError_t stream_scratch(hipStream_t s, size_t bytes, void** out);
 hipError_t occupancy(int* per_cu, const void* kern, int block, size_t lds);
 const char* acc_name(int acc);
 int pool_tiles(int pix, int xc, int rows);

@@ -48,6 +48,17 @@ int order_used(Context::TileOrder& e, hipStream_t s) {
     LRT_HIP(hipEventRecord(ev, s));
     return LRT_OK;
 }
+// Stream s waits for entry e's recording launch and sort -- until they are seen complete, after
+// which no launch needs the wait (one command fewer between a stream's kernels).
+int order_wait(Context::TileOrder& e, hipStream_t s) {
+    if (!e.rec_done) {
+        const hipError_t q = hipEventQuery(e.ev_rec);
+        if (q == hipSuccess) e.rec_done = true;
+        else if (q != hipErrorNotReady) return hip_fail(q, "hipEventQuery(tile order)");
+    }
+    if (!e.rec_done) LRT_HIP(hipStreamWaitEvent(s, e.ev_rec, 0));
+    return LRT_OK;
+}
 // Picks a's order for this launch: a.perm (null: queue order) and, for the recording launch,
 // a.tcost. *users gets the entries whose buffers the launch touches (order_used after it).
 // LRT_POOL_PROBE: 0 off; 1 (default) a new signature without an order of the same geometry
@@ -140,17 +151,18 @@ int tile_order(KernelArgs& a, int kPix, long long ntiles, bool& record, Context:
         // the recording launch writes d_cost and the sort behind it (launch_pool) d_perm:
         // ready for every later launch once ev_rec has passed, which each of them waits for
         e->state = 2;
+        e->rec_done = false;
         e->donor = donor;
         a.tcost = e->d_cost;
         record = true;
         if (donor >= 0) {   // meanwhile the newest order of the same geometry
             users[1] = &c.order[donor];
-            LRT_HIP(hipStreamWaitEvent(s, users[1]->ev_rec, 0));
+            if (int rc = order_wait(*users[1], s)) return rc;
             a.perm = users[1]->d_perm;
             users[1]->tick = ++c.order_tick;
         }
     } else {
-        LRT_HIP(hipStreamWaitEvent(s, e->ev_rec, 0));
+        if (int rc = order_wait(*e, s)) return rc;
         a.perm = e->d_perm;
     }
     users[0] = e;

@@ -8,7 +8,7 @@ namespace lrt {
 
 // Waves per block of the grid instance (kPoolGridWaves blocks share the grid's LDS copy); 1
 // when the grid does not fit beside the waves' stacks.
-inline int pool_grid_wpb(const KernelArgs& a, size_t stack_w, size_t shared_b, size_t* grid_b) {
+inline int pool_grid_wpb(const KernelArgs& a, size_t stack_w, size_t shared_b, size_t static_b, size_t* grid_b) {
     const size_t ncell = (size_t)a.gv.nx * a.gv.ny * a.gv.nz, nref = a.gv.cells_refs;
     *grid_b = (16 * nref + 8 * ncell + 4 * nref + 15) / 16 * 16;
     if (!a.gv.on || a.gv.nx == 0) return 1;
@@ -16,7 +16,7 @@ inline int pool_grid_wpb(const KernelArgs& a, size_t stack_w, size_t shared_b, s
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&maxb, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess)
         return 1;
-    return kPoolGridWaves * stack_w + shared_b + *grid_b <= (size_t)maxb ? kPoolGridWaves : 1;
+    return kPoolGridWaves * stack_w + shared_b + *grid_b + static_b <= (size_t)maxb ? kPoolGridWaves : 1;
 }
 
 template <int MAXD, int kPix>
@@ -29,9 +29,15 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     const size_t bstk = acc == kAccBvh ? sizeof(unsigned short) * ctx().bvh_stack_levels * 64
                         : acc == kAccGrid ? (sizeof(float4) + sizeof(int)) * (size_t)a.gv.nbig : 0;
     size_t grid_b = 0;
+    // the instance's static LDS (diagnostic builds' section counters) beside the dynamic
+    static const size_t static_b = [] {
+        hipFuncAttributes fa{};
+        return hipFuncGetAttributes(&fa, (const void*)pool_kernel<MAXD, false, kAccGrid, kPix, 0, kW>) == hipSuccess
+                   ? fa.sharedSizeBytes
+                   : (size_t)0;
+    }();
     int wpb = acc == kAccGrid && !lds
-                  ? pool_grid_wpb(a, pool_stack_bytes<kW>(),
-                                  kPowTableBytes + (bstk + 15) / 16 * 16, &grid_b)
+                  ? pool_grid_wpb(a, pool_stack_bytes<kW>(), kPowTableBytes + (bstk + 15) / 16 * 16, static_b, &grid_b)
                   : 1;
     if (wpb > 1) {
         // dynamic LDS above the default limit: raised once per device for this instance
@@ -42,7 +48,8 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
         if (r && *r == 0)
             *r = hipDeviceGetAttribute(&maxb, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) == hipSuccess &&
                          hipFuncSetAttribute((const void*)pool_kernel<MAXD, false, kAccGrid, kPix, 0, kW>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, maxb) == hipSuccess
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             maxb - (int)static_b) == hipSuccess
                      ? 1
                      : -1;
         if (!r || *r < 0) wpb = 1;
@@ -83,14 +90,18 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     a.regenMin = 16;
     a.poolSlots = kPix * std::min(a.frames, kPoolSamples / kPix);   // one round's samples
     const size_t nwaves = (size_t)grid.x * wpb;
-    e = hipMallocAsync((void**)&a.colbuf, sizeof(float) * 3 * (size_t)a.poolSlots * nwaves, s);
-    if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(pool colour slots)");
-    if (a.maxDepth > lv) {
-        const size_t gthreads = nwaves * 64;
-        // float4 levels, then the u16 level tags (lrt_pool.h)
-        e = hipMallocAsync((void**)&a.ovf, (sizeof(float4) + sizeof(unsigned short)) * gthreads *
-                                               (size_t)(a.maxDepth - lv), s);
-        if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(trace stack overflow)");
+    // the colour slots, then the overflow stack's float4 levels and u16 level tags (lrt_pool.h),
+    // in the stream's scratch (kept between launches)
+    const size_t col_b = (sizeof(float) * 3 * (size_t)a.poolSlots * nwaves + 255) / 256 * 256;
+    const size_t ovf_b = a.maxDepth > lv ? (sizeof(float4) + sizeof(unsigned short)) * nwaves * 64 *
+                                               (size_t)(a.maxDepth - lv)
+                                         : 0;
+    {
+        void* p = nullptr;
+        e = stream_scratch(s, col_b + ovf_b, &p);
+        if (e != hipSuccess) return hip_fail(e, "pool scratch (colour slots, overflow stack)");
+        a.colbuf = static_cast<float*>(p);
+        if (ovf_b) a.ovf = reinterpret_cast<float4*>(static_cast<char*>(p) + col_b);
     }
 #ifdef LRT_EXP_SECSTATS
     unsigned long long* d_sec = secstats_buffer(s);
@@ -161,12 +172,6 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
 #ifdef LRT_EXP_WAVETRACE
     wavetrace_dump(a.wtrace, grid.x, s);
 #endif
-    e = hipFreeAsync(a.colbuf, s);
-    if (e != hipSuccess) return hip_fail(e, "hipFreeAsync(pool colour slots)");
-    if (a.ovf) {
-        e = hipFreeAsync(a.ovf, s);
-        if (e != hipSuccess) return hip_fail(e, "hipFreeAsync(trace stack overflow)");
-    }
     return LRT_OK;
 }
 

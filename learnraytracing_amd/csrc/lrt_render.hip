@@ -120,6 +120,42 @@ void secstats_dump(const unsigned long long* d_sec, hipStream_t s) {
 #endif
 
 
+hipError_t stream_scratch(hipStream_t s, size_t bytes, void** out) {
+    Context& c = ctx();
+    Context::Scratch* hit = nullptr;
+    for (auto& e : c.scratch)
+        if (e.p && e.s == s) hit = &e;
+    if (!hit) {   // a free slot, or the least recently used one (its stream may be gone: a full sync)
+        hit = &c.scratch[0];
+        for (auto& e : c.scratch)
+            if (!e.p || (hit->p && e.tick < hit->tick)) hit = &e;
+        if (hit->p) {
+            hipError_t e = hipDeviceSynchronize();
+            if (e == hipSuccess) e = hipFree(hit->p);
+            if (e != hipSuccess) return e;
+        }
+        *hit = Context::Scratch();
+        hit->s = s;
+    }
+    if (hit->bytes < bytes) {   // grow, ordered on the stream that uses it
+        if (hit->p) {
+            const hipError_t e = hipFreeAsync(hit->p, s);
+            hit->p = nullptr;
+            hit->bytes = 0;
+            if (e != hipSuccess) return e;
+        }
+        const hipError_t e = hipMallocAsync(&hit->p, bytes, s);
+        if (e != hipSuccess) {
+            hit->p = nullptr;
+            return e;
+        }
+        hit->bytes = bytes;
+    }
+    hit->tick = ++c.order_tick;
+    *out = hit->p;
+    return hipSuccess;
+}
+
 // Resident blocks per CU for (kernel, LDS bytes), cached: the query costs host time on
 // every launch otherwise.
 hipError_t occupancy(int* per_cu, const void* kern, int block, size_t lds) {

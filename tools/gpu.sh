@@ -20,6 +20,8 @@ out=gpurun_out/$TAG
 mkdir -p "$out"
 export TMPDIR=/tmp
 BSTEPS=${BSTEPS:-20}
+STEPARG=(--steps "$BSTEPS")
+[ "$BSTEPS" = default ] && STEPARG=()   # bench.py's per-config default
 declare -A PMC=(
   [fetch]="FETCH_SIZE"
   [write]="WRITE_SIZE"
@@ -55,9 +57,9 @@ for s in "$@"; do
         run "test$i" 1100 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread
       fi ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    bench) TAILN=1 run "bench_c${c}_$i" 600 python bench.py --config "$c" --steps "$BSTEPS" $extra ;;
+    bench) TAILN=1 run "bench_c${c}_$i" 600 python bench.py --config "$c" "${STEPARG[@]}" $extra ;;
     trace) run "trace_c${c}_$i" 600 rocprofv3 --kernel-trace --stats -d "$out" -o "trace_c${c}" --output-format csv -- \
-             python3 bench.py --config "$c" --steps "$BSTEPS" --streams 1 --no-cpu-baseline $extra ;;
+             python3 bench.py --config "$c" "${STEPARG[@]}" --streams 1 --no-cpu-baseline $extra ;;
     pmc)   g=${rest%%,*}
            pextra=""
            [[ "$rest" == *,* ]] && pextra=${rest#*,}
@@ -78,7 +80,7 @@ for s in "$@"; do
              if [[ "$tok" =~ ^[A-Z_][A-Z0-9_]*= ]]; then envs+=("$tok"); else bargs+=("$tok"); fi
            done
            TAILN=1 run "ab_${c}_c${c2}_$i" 600 env LRT_LIB="$lib" "${envs[@]}" python bench.py --config "$c2" \
-             --steps "$BSTEPS" --no-cpu-baseline --no-extra-legs "${bargs[@]}" ;;
+             "${STEPARG[@]}" --no-cpu-baseline --no-extra-legs "${bargs[@]}" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
