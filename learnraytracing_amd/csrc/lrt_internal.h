@@ -65,11 +65,6 @@ constexpr int kWavesPerEU = 4;
 // round. Config 4 (64 spp): 1024 (16 px) 229 ms, 2048 (32 px) 222, 4096 (64 px) 221;
 // config 5 (256 spp, one GPU): 1024 (4 px) 3876 ms, 4096 (16 px) 3602 (profiles/r2_p2).
 constexpr int kPoolSamples = 4096;
-#ifdef LRT_EXP_ROUND_SAMPLES
-constexpr int kRoundSamples = LRT_EXP_ROUND_SAMPLES;
-#else
-constexpr int kRoundSamples = kPoolSamples;
-#endif
 
 struct KernelArgs {
     CameraDev cam;

@@ -216,7 +216,7 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
     float* const slots = a.colbuf + (size_t)wid * a.poolSlots * 3;
 
     constexpr int TX = PoolTile<kPix>::X, TY = PoolTile<kPix>::Y;
-    constexpr int kRoundFrames = kRoundSamples / kPix > 0 ? kRoundSamples / kPix : 1;
+    constexpr int kRoundFrames = kPoolSamples / kPix;
     const int tilesX = (a.xc + TX - 1) / TX;
     const int ntiles = tilesX * ((a.rows + TY - 1) / TY);
     const float invWidth = 1.0f / (float)a.width;     // parallel.cpp:260

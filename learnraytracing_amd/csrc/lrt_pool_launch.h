@@ -88,7 +88,7 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     // waiting lanes that trigger a refill (fold + next samples). Measured (profiles/r2_p2):
     // config 3 2.31 -> 2.05 ms/step at 16 (vs 1), config 4 and config 2 neutral
     a.regenMin = 16;
-    a.poolSlots = kPix * std::min(a.frames, std::max(1, kRoundSamples / kPix));   // one round's samples
+    a.poolSlots = kPix * std::min(a.frames, kPoolSamples / kPix);   // one round's samples
     const size_t nwaves = (size_t)grid.x * wpb;
     // the colour slots, then the overflow stack's float4 levels and u16 level tags (lrt_pool.h),
     // in the stream's scratch (kept between launches)
