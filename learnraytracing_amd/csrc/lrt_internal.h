@@ -164,7 +164,10 @@ struct Context {
         unsigned* d_cost = nullptr;    // written by the recording launch
         unsigned* d_keys = nullptr;
         int* d_ids = nullptr;          // 0..cap-1
-        int* d_perm = nullptr;         // written once (by the sort), read by every later launch
+        int* d_perm = nullptr;         // the live permutation, read by every later launch
+        int* d_permb[2] = {nullptr, nullptr};   // its two buffers (the refining pass sorts into the other)
+        int* d_sort_out = nullptr;     // where the sort behind the current recording launch writes
+        int passes = 0;                // recording launches so far (1: the first; 2: refined)
         void* d_tmp = nullptr;
         size_t tmp_bytes = 0;
         hipEvent_t ev_rec = nullptr;   // after the recording launch and the sort behind it
@@ -376,7 +379,8 @@ int launch_pool_d64(const KernelArgs& a, bool lds, int xc, int rows, int frames,
 bool pool_order_on();
 int pool_probe_mode();
 int order_used(Context::TileOrder& e, hipStream_t s);
-int tile_order(KernelArgs& a, int kPix, long long ntiles, bool& record, Context::TileOrder* users[2], hipStream_t s);
+// record: 0 none, 1 the signature's first recording launch, 2 its refining pass (tile_order)
+int tile_order(KernelArgs& a, int kPix, long long ntiles, int& record, Context::TileOrder* users[2], hipStream_t s);
 // the tile-cost probe of a recording launch: costs into o.d_cost, heaviest-first into o.d_perm
 hipError_t launch_tile_probe(const KernelArgs& a, int acc, Context::TileOrder& o, int ntiles, int TX, int TY,
                              size_t bstk, hipStream_t s);

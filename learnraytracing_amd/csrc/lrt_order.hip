@@ -80,11 +80,11 @@ int order_alloc(Context::TileOrder& e, long long ntiles, hipStream_t s) {
     const long long cap = std::max(ntiles, 65536LL);
     size_t tmp = 0;
     LRT_HIP(sort_tiles_desc(nullptr, nullptr, nullptr, nullptr, (int)cap, nullptr, &tmp, s));
-    const size_t arr = ((size_t)cap * 4 + 255) & ~(size_t)255;
+    const size_t arr = ((size_t)cap * 4 + 255) & ~(size_t)255;   // cost, keys, ids, two perms
     if (e.d_base) (void)hipFree(e.d_base);   // (its launches have passed: order_release)
     e.d_base = nullptr;
     e.cap = 0;
-    if (hipMalloc(&e.d_base, 4 * arr + tmp) != hipSuccess) {
+    if (hipMalloc(&e.d_base, 5 * arr + tmp) != hipSuccess) {
         e.d_base = nullptr;
         return fail(LRT_E_NOMEM, "hipMalloc(tile order)");
     }
@@ -92,8 +92,10 @@ int order_alloc(Context::TileOrder& e, long long ntiles, hipStream_t s) {
     e.d_cost = reinterpret_cast<unsigned*>(b);
     e.d_keys = reinterpret_cast<unsigned*>(b + arr);
     e.d_ids = reinterpret_cast<int*>(b + 2 * arr);
-    e.d_perm = reinterpret_cast<int*>(b + 3 * arr);
-    e.d_tmp = b + 4 * arr;
+    e.d_permb[0] = reinterpret_cast<int*>(b + 3 * arr);
+    e.d_permb[1] = reinterpret_cast<int*>(b + 4 * arr);
+    e.d_perm = e.d_permb[0];
+    e.d_tmp = b + 5 * arr;
     e.tmp_bytes = tmp;
     LRT_HIP(fill_iota(e.d_ids, (int)cap, s));
     // a later signature may take this entry on another stream, whose sort reads d_ids: the
@@ -103,8 +105,8 @@ int order_alloc(Context::TileOrder& e, long long ntiles, hipStream_t s) {
     return LRT_OK;
 }
 
-int tile_order(KernelArgs& a, int kPix, long long ntiles, bool& record, Context::TileOrder* users[2], hipStream_t s) {
-    record = false;
+int tile_order(KernelArgs& a, int kPix, long long ntiles, int& record, Context::TileOrder* users[2], hipStream_t s) {
+    record = 0;
     users[0] = users[1] = nullptr;
     if (!pool_order_on() || ntiles < 2 * kV0Queues) return LRT_OK;
     Context& c = ctx();
@@ -153,8 +155,11 @@ int tile_order(KernelArgs& a, int kPix, long long ntiles, bool& record, Context:
         e->state = 2;
         e->rec_done = false;
         e->donor = donor;
+        e->passes = 1;
+        e->d_perm = e->d_permb[0];
+        e->d_sort_out = e->d_perm;
         a.tcost = e->d_cost;
-        record = true;
+        record = 1;
         if (donor >= 0) {   // meanwhile the newest order of the same geometry
             users[1] = &c.order[donor];
             if (int rc = order_wait(*users[1], s)) return rc;
@@ -164,6 +169,20 @@ int tile_order(KernelArgs& a, int kPix, long long ntiles, bool& record, Context:
     } else {
         if (int rc = order_wait(*e, s)) return rc;
         a.perm = e->d_perm;
+        if (e->passes == 1) {
+            // The refining pass: this launch takes its tiles in the first pass's order and records
+            // them again. The first pass timed each tile in queue order, where a tile's wall time
+            // depends on where in the launch it ran; timed in the sorted order, the heavy tiles run
+            // together at the start and the light ones at the end, as every later launch runs them
+            // (profiles/r5_x). Its sort writes the other permutation buffer: launches still reading
+            // this one are untouched, later ones wait for the sort (ev_rec) and read the new one.
+            e->passes = 2;
+            e->rec_done = false;
+            e->d_sort_out = e->d_permb[e->d_perm == e->d_permb[0] ? 1 : 0];
+            e->d_perm = e->d_sort_out;
+            a.tcost = e->d_cost;
+            record = 2;
+        }
     }
     users[0] = e;
     e->tick = ++c.order_tick;

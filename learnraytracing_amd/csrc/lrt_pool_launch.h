@@ -110,11 +110,11 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
 #ifdef LRT_EXP_WAVETRACE
     a.wtrace = wavetrace_buffer((unsigned)nwaves);
 #endif
-    bool record = false;
+    int record = 0;
     Context::TileOrder* users[2];
     if (int rc = tile_order(a, kPix, ntiles, record, users, s)) return rc;
     bool probed = false;
-    if (record && pool_probe_mode() > 0 && (pool_probe_mode() == 2 || !users[1])) {
+    if (record == 1 && pool_probe_mode() > 0 && (pool_probe_mode() == 2 || !users[1])) {
         // no measured order to go by: probe the tiles' costs, sort them, and let this
         // (recording) launch take its tiles in that order (probe_kernel, lrt_pool.h)
         Context::TileOrder& o = *users[0];
@@ -149,7 +149,7 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     }
     if (record) {   // the costs just recorded, sorted on the device behind the launch
         Context::TileOrder& o = *users[0];
-        e = sort_tiles_desc(o.d_cost, o.d_keys, o.d_ids, o.d_perm, (int)ntiles, o.d_tmp, &o.tmp_bytes, s);
+        e = sort_tiles_desc(o.d_cost, o.d_keys, o.d_ids, o.d_sort_out, (int)ntiles, o.d_tmp, &o.tmp_bytes, s);
         if (e == hipSuccess) e = hipEventRecord(o.ev_rec, s);
         if (e != hipSuccess) {
             o.state = 0;   // no order for this signature: the next launch records again
@@ -161,11 +161,11 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
             if (int rc = order_used(*u, s)) return rc;
     // order: 0 queue order (tile order off), 1 recording in queue order, 2 the signature's own
     // sorted order, 3 recording with the order borrowed from the same geometry, 4 recording in
-    // the probe's order
+    // the probe's order, 5 the refining pass (recording in the first pass's sorted order)
     snprintf(g_last_launch, sizeof(g_last_launch),
              "kernel=pool_kernel maxd=%d lds=%d bvh=%d acc=%s pix=%d ns=%d grid=%u tasks=%lld order=%d per_cu=%d wpb=%d",
              MAXD, lds ? 1 : 0, acc == kAccBvh ? 1 : 0, acc_name(acc), kPix, fixed ? kFixedSpheres : 0, grid.x, ntiles,
-             !users[0] ? 0 : !record ? 2 : probed ? 4 : users[1] ? 3 : 1, per_cu, wpb);
+             !users[0] ? 0 : !record ? 2 : record == 2 ? 5 : probed ? 4 : users[1] ? 3 : 1, per_cu, wpb);
 #ifdef LRT_EXP_SECSTATS
     secstats_dump(d_sec, s);
 #endif

@@ -216,8 +216,9 @@ def test_pool_order_two_streams_bitwise(gpu):
     """The bench's pipelining: config 2 launched alternately on two streams, each into its own
     buffer, across the recording launch and the switch to the heaviest-first order, with no
     host synchronisation in between: the order is sorted on the device behind the recording
-    launch, and every later launch, on either stream, waits for that sort's event. Every frame
-    equals the single-stream render."""
+    launch, the second launch (the other stream) records again in that order and sorts into the
+    other permutation buffer (order=5), and every later launch, on either stream, waits for the
+    latest sort's event. Every frame equals the single-stream render."""
     import torch
     from learnraytracing_amd import _lib as L
     w, h = 1280, 720
@@ -233,7 +234,7 @@ def test_pool_order_two_streams_bitwise(gpu):
     want, _ = oracle.orc_render(w, h, 4, 8, cam22=cam.to22())
     for k, o in enumerate(outs):
         _bitwise(o.cpu().numpy(), want, f"launch {k} (order {orders[k]})")
-    assert orders[0] in ("1", "3", "4") and orders[1:] == ["2"] * 7, orders
+    assert orders[0] in ("1", "3", "4") and orders[1] == "5" and orders[2:] == ["2"] * 6, orders
 
 
 def test_config2_benchmarked_state_vs_oracle(gpu):
@@ -245,7 +246,8 @@ def test_config2_benchmarked_state_vs_oracle(gpu):
     job = gpu.Job(width=w, height=h, frames=4, max_depth=8)
     s = torch.cuda.current_stream()
     warm = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
-    _torch_render(gpu, job, s, warm)
+    for _ in range(2):   # the recording launch and the refining pass
+        _torch_render(gpu, job, s, warm)
     torch.cuda.synchronize()
     out = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
     rays = _torch_render(gpu, job, s, out)
@@ -264,7 +266,7 @@ def test_new_view_borrows_order_bitwise(gpu):
     w, h = 1280, 720
     # (flags 512: the pool kernel; a host buffer of <= 4 frames otherwise takes the pipelined
     # host path, whose colours v0 renders)
-    for _ in range(2):   # view A: recording launch, then its own order
+    for _ in range(3):   # view A: recording launch, the refining pass, then its own order
         _host(gpu, gpu.Job(width=w, height=h, frames=4, max_depth=8, flags=512))
     assert L.last_launch()["order"] == "2"
     cam = gpu.make_camera((0.3, 2.1, 3), (0, 0, 0), (0, 1, 0), 60, w / h, 0.1, 3)
@@ -278,12 +280,12 @@ def test_new_view_borrows_order_bitwise(gpu):
 def test_probe_ordered_first_launch_vs_oracle(gpu):
     """A geometry with no measured order yet (this window's shape is used by no other test):
     the first launch takes its tiles in the cost probe's order (probe_kernel +
-    probe_order_kernel, order=4), the second in its own measured order; both are the
-    restatement's pixels and ray count."""
+    probe_order_kernel, order=4), the second in its own measured order while it records again
+    (order=5), the third in the refined order; all are the restatement's pixels and ray count."""
     from learnraytracing_amd import _lib as L
     kw = dict(width=1280, height=720, frames=4, max_depth=8, x0=100, x_count=312, y0=200, row_count=104)
     want, wrays = oracle.orc_render(1280, 720, 4, 8, 0, 100, 312, 200, 104, threads=16)
-    for order in ("4", "2"):
+    for order in ("4", "5", "2"):
         buf, rays = _host(gpu, gpu.Job(flags=512, **kw))
         info = L.last_launch()
         assert info["kernel"] == "pool_kernel" and info["order"] == order, info
@@ -297,7 +299,8 @@ def test_config3_full_frame_vs_oracle(gpu):
     launch): bit-exact vs the C oracle."""
     from learnraytracing_amd import _lib as L
     job = gpu.Job(width=1920, height=1080, frames=16, max_depth=50)
-    _host(gpu, job)
+    _host(gpu, job)   # the recording launch
+    _host(gpu, job)   # the refining pass
     buf, rays = _host(gpu, job)
     info = L.last_launch()
     assert info["kernel"] == "pool_kernel" and info["maxd"] == "64" and info["order"] == "2", info

@@ -64,7 +64,7 @@ for s in "$@"; do
            pextra=""
            [[ "$rest" == *,* ]] && pextra=${rest#*,}
            run "pmc_c${c}_$g" 300 rocprofv3 --pmc ${PMC[$g]} -d "$out" -o "pmc_c${c}_$g" --output-format csv -- \
-             python3 bench.py --config "$c" --steps 2 --warmup 1 --streams 1 --no-cpu-baseline --no-extra-legs ${pextra//;/ } ;;
+             python3 bench.py --config "$c" --steps 2 --warmup 2 --streams 1 --no-cpu-baseline --no-extra-legs ${pextra//;/ } ;;
     py)    penv=() pargs=()   # NAME=VALUE tokens are environment settings (e.g. LRT_LIB=...)
            for tok in ${val//,/ }; do
              if [[ "$tok" =~ ^[A-Z_][A-Z0-9_]*= ]]; then penv+=("$tok"); else pargs+=("$tok"); fi
