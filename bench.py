@@ -23,8 +23,11 @@ parallel.cpp:122,204). Inputs are resident in HBM (the scene is uploaded once); 
 host transfer is inside the timed region.
 
 Besides the timed region (unless --no-extra-legs):
-  * `ms_per_launch_alone`: the same launches one at a time on one stream, each bracketed
-    by HIP events on that stream -- the duration the roofline objects divide by;
+  * `ms_per_launch_alone`: the same launches one at a time on one stream, each kernel
+    bracketed by HIP events the library records on that stream right around it
+    (lrt_kernel_timing) -- the duration the roofline objects divide by; `ms_per_call_alone`:
+    the same launches with the events around the whole render call (its other stream
+    commands and dispatch included);
   * `end_to_end`: render (+ gather and assembly) + the D2H copy of the frame into pinned
     host memory on rank 0, pipelined over two slots;
   * `cpu_baseline` (all host cores) and `cpu_baseline_1core`: the reference's own
@@ -35,6 +38,7 @@ Rank 0 prints ONE JSON line on stdout; progress goes to stderr.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -533,13 +537,14 @@ def main():
     remote = mode == "remote"
 
     # ---- extra legs: each launch alone (roofline duration), end to end (D2H included)
-    alone_ms = e2e_s = None
+    alone_ms = e2e_s = call_ms = None
     e2e_steps = 0
     if extra:
         wd.enter("launch_alone")
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.steps)]
         scratch = torch.zeros(1, dtype=torch.int64, device=dev)
+        L.check(L.lib().lrt_kernel_timing(1))
         for k in range(args.steps):
             ev[k][0].record(stream)
             if remote:
@@ -548,7 +553,13 @@ def main():
                 lrt.render_tensor(job, bufs[0], scratch, stream)
             ev[k][1].record(stream)
         torch.cuda.synchronize()
-        alone_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+        call_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+        kt = (ctypes.c_float * args.steps)()
+        nk = ctypes.c_int(0)
+        L.check(L.lib().lrt_kernel_times(kt, args.steps, ctypes.byref(nk)))
+        L.check(L.lib().lrt_kernel_timing(0))
+        # one render kernel per launch: the kernel's own events; else the call's
+        alone_ms = sum(kt[:nk.value]) / nk.value if nk.value == args.steps else call_ms
         if rank == 0:
             shape = (H, W, 4) if world > 1 else tuple(bufs[0].shape)   # --shard-of: the shard itself
             host = [torch.empty(shape, dtype=torch.float32, pin_memory=True) for _ in range(nslots)]
@@ -677,6 +688,7 @@ def main():
             "warmup": warmup,
             "ms_per_step": round(ms_step, 4),
             "ms_per_launch_alone": round(alone_ms, 4) if alone_ms else None,
+            "ms_per_call_alone": round(call_ms, 4) if call_ms else None,
             "higher_is_better": True,
             "scaling": args.scaling,
             "vs_baseline": None,

@@ -137,6 +137,8 @@ SIGNATURES = {
     "lrt_bvh_stats": (_i, [_c.POINTER(Sphere), _i, _vp, _i, _vp]),
     "lrt_grid_stats": (_i, [_c.POINTER(Sphere), _i, _vp, _i, _vp]),
     "lrt_accel_eval": (_i, [_c.POINTER(Sphere), _i, _vp, _i, _i, _i, _vp, _vp]),
+    "lrt_kernel_timing": (_i, [_i]),
+    "lrt_kernel_times": (_i, [_vp, _i, _vp]),
     "lrt_scatter_eval": (_i, [_c.POINTER(Sphere), _c.POINTER(Material), _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp,
                               _vp, _i]),
 }

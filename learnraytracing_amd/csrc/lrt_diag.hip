@@ -89,6 +89,28 @@ __global__ __launch_bounds__(64) void accel_probe_kernel(BvhView bv, GridView g,
 
 using namespace lrt;
 
+namespace lrt {
+bool g_ktiming_on = false;
+std::vector<std::pair<hipEvent_t, hipEvent_t>> g_ktiming_ev;   // (start, stop) per recorded launch
+size_t g_ktiming_used = 0;
+void kernel_timing_mark(hipStream_t s, int which) {
+    if (which == 0) {
+        if (g_ktiming_used == g_ktiming_ev.size()) {
+            hipEvent_t a = nullptr, b = nullptr;
+            if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
+                g_ktiming_on = false;   // (diagnostic only: stop rather than fail the render)
+                return;
+            }
+            g_ktiming_ev.emplace_back(a, b);
+        }
+        (void)hipEventRecord(g_ktiming_ev[g_ktiming_used].first, s);
+    } else {
+        (void)hipEventRecord(g_ktiming_ev[g_ktiming_used].second, s);
+        ++g_ktiming_used;
+    }
+}
+}  // namespace lrt
+
 extern "C" {
 
 // Diagnostic (host only, no GPU): build the BVH of the given scene and trace n rays
@@ -401,4 +423,25 @@ int lrt_libm_eval_device(int kind, const float* d_in, float* d_out, long long n)
     return LRT_OK;
 }
 
+
+// ---- kernel timing (lrt_kernel_timing) ----------------------------------------------------
+int lrt_kernel_timing(int on) {
+    lrt::g_ktiming_on = on != 0;
+    lrt::g_ktiming_used = 0;
+    return LRT_OK;
+}
+int lrt_kernel_times(float* ms, int max_n, int* n) {
+    if (!n || (max_n > 0 && !ms)) return lrt::fail(LRT_E_INVALID, "lrt_kernel_times: null output");
+    int k = 0;
+    for (size_t i = 0; i < lrt::g_ktiming_used && k < max_n; ++i) {
+        auto& p = lrt::g_ktiming_ev[i];
+        LRT_HIP(hipEventSynchronize(p.second));
+        float t = 0.0f;
+        LRT_HIP(hipEventElapsedTime(&t, p.first, p.second));
+        ms[k++] = t;
+    }
+    *n = k;
+    lrt::g_ktiming_used = 0;
+    return LRT_OK;
+}
 }  // extern "C"

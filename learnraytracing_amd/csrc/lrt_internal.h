@@ -346,6 +346,12 @@ int camera_default(int w, int h, lrt_camera* out);
 int validate(const lrt_render_desc* d);
 // At least `bytes` of device scratch for launches on stream s (Context::scratch).
 hipError_t stream_scratch(hipStream_t s, size_t bytes, void** out);
+// lrt_kernel_timing (lrt_diag.h): events right around each render kernel launch on its stream
+extern bool g_ktiming_on;
+void kernel_timing_mark(hipStream_t s, int which);   // 0 before the kernel, 1 after
+inline void kernel_timing(hipStream_t s, int which) {
+    if (g_ktiming_on) kernel_timing_mark(s, which);
+}
 hipError_t occupancy(int* per_cu, const void* kern, int block, size_t lds);
 const char* acc_name(int acc);
 int pool_tiles(int pix, int xc, int rows);

@@ -129,6 +129,7 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
         users[1] = nullptr;   // (a borrowed order, if any, is not used)
         probed = true;
     }
+    kernel_timing(s, 0);
     if (acc == kAccGrid) {
         if (lds) pool_kernel<MAXD, true, kAccGrid, kPix><<<grid, 64, ldsb, s>>>(a);
         else if (wpb > 1) pool_kernel<MAXD, false, kAccGrid, kPix, 0, kW><<<grid, 64 * kW, ldsb, s>>>(a);
@@ -142,6 +143,7 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
         if (lds) pool_kernel<MAXD, true, kAccScan, kPix><<<grid, 64, ldsb, s>>>(a);
         else pool_kernel<MAXD, false, kAccScan, kPix><<<grid, 64, ldsb, s>>>(a);
     }
+    kernel_timing(s, 1);
     e = hipGetLastError();
     if (e != hipSuccess) {
         if (record) users[0]->state = 0;   // nothing recorded: the entry is free again

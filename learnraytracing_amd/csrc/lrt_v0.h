@@ -327,6 +327,7 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
         e = hipMallocAsync((void**)&a.ovf, sizeof(float4) * gthreads * (size_t)(a.maxDepth - kTraceLdsLevels), s);
         if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(trace stack overflow)");
     }
+    kernel_timing(s, 0);
     if constexpr (!kFeat && (kSplit >= 4 || kSplit == 1)) {
         if (samp && a.sampOnly) {   // the caller lerps the planes (render_host's pipeline)
             if (fixed)
@@ -369,6 +370,7 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
         else
             trace_kernel<MAXD, false, false, kSplit, kFeat><<<grid, kBlock, ldsb, s>>>(a);
     }
+    kernel_timing(s, 1);
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "trace_kernel launch");
     snprintf(g_last_launch, sizeof(g_last_launch),
