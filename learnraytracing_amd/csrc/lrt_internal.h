@@ -92,6 +92,7 @@ struct KernelArgs {
     float4* feat[6];
     int featMax;
     int regenMin;                 // v5: waiting lanes that trigger a refill
+    int lateFetch;                // v5: reserve the next tile at this one's end, not its start (lrt_pool.h)
     const float* lerp;            // lerpFac = (float)f / (float)(f + 1) for f < kLerpTable (parallel.cpp:262)
     float4* samp;                 // sample mode: frames planes of xc * rows colours
     float* colbuf;                // v5 (pool): poolSlots colour slots (RGB) per block

@@ -239,8 +239,19 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
         ++wtiles;
 #endif
         const int tx0 = (tile % tilesX) * TX, ty0 = (tile / tilesX) * TY;
+        // The next tile is reserved (queue atomic) at this tile's start, which hides the atomic's
+        // latency behind the whole tile -- or, in launches of few tiles per wave (a.lateFetch:
+        // config 2 has 3.5), once this tile's last samples are handed out: a tile reserved at the
+        // start of the one before it is held by a wave still a whole tile away from it, and at the
+        // launch's end the queue's last tiles waited for such waves while others found the queue
+        // empty (profiles/r5_m). Config 2 alone 0.272 -> 0.259 ms, two streams within noise
+        // (profiles/r5_z); with many tiles per wave the exposed latency costs more than the tail
+        // (configs 3-4: +1-2 %, r5_n); only the depth-8 one-wave instances carry the code (its
+        // presence alone cost config 3's instance 0.9 %, r5_aa).
+        constexpr bool kLate = kW == 1 && MAXD <= 8;
         unsigned long long fetched = 0;
-        if (lane == 0) fetched = atomicAdd(ctr, 1ull);   // consumed after the tile (hides its latency)
+        bool asked = !(kLate && a.lateFetch);
+        if (asked && lane == 0) fetched = atomicAdd(ctr, 1ull);   // consumed after the tile
         for (int fr0 = a.frame0; fr0 < fend; fr0 += kRoundFrames) {
             const int nfr = fend - fr0 < kRoundFrames ? fend - fr0 : kRoundFrames;
             const int N = nfr * kPix;   // this round's pool
@@ -307,6 +318,12 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
                         }
                     }
                     next += __popcll(needM);
+                    if constexpr (kLate) {
+                        if (!asked && next >= N && fr0 + kRoundFrames >= fend) {   // the tile's last samples
+                            if (lane == 0) fetched = atomicAdd(ctr, 1ull);
+                            asked = true;
+                        }
+                    }
                 }
                 const unsigned long long traceM = __ballot(state == kPoolTrace);
                 if (traceM == 0) {
@@ -436,6 +453,8 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
         // recording launch: the tile's cost = its wall time (the rays it traced ordered config 2
         // worse: 0.300 against 0.276 ms alone, profiles/r5_p)
         if (a.tcost && lane == 0) a.tcost[tile] = (unsigned)(__builtin_amdgcn_s_memrealtime() - tt0);
+        if constexpr (kLate)
+            if (!asked && lane == 0) fetched = atomicAdd(ctr, 1ull);   // (a tile whose pool never ran dry)
         const unsigned long long n = __shfl(fetched, 0, 64) + (unsigned long long)bq;
         i = n < (unsigned long long)nq ? (int)n : nq;
     }

@@ -373,6 +373,7 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     // round-1 per-lane state machines (v1/v2/v2s) and round-1's v3 regeneration kernel (slower
     // than v0 or v5 on every config) were removed: their flags are rejected.
     a.regenMin = 0;
+    a.lateFetch = 0;
     a.lerp = ctx().d_lerp;
     a.colbuf = nullptr;
     a.poolSlots = 0;
