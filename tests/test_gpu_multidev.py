@@ -360,3 +360,50 @@ def test_probe_order_many_tiles_equals_v0(gpu):
     assert L.last_launch()["kernel"] == "trace_kernel"
     _bitwise(buf, want, "probe order over 21,120 tiles vs v0")
     assert rays == wrays
+
+
+def test_pool_scratch_grows_and_is_reused_bitwise(gpu):
+    """The pool kernel's colour slots and overflow stack live in a per-stream scratch buffer kept
+    between launches (lrt_render.hip stream_scratch): a small window, then windows that need more
+    (more waves' slots; a 20-bounce budget with overflow levels), then the small one again, all on
+    one stream: every render is the restatement's."""
+    import torch
+    from learnraytracing_amd import _lib as L
+    s = torch.cuda.Stream()
+    cases = [dict(x0=0, x_count=320, y0=0, row_count=64, max_depth=8),
+             dict(x0=0, x_count=1280, y0=0, row_count=360, max_depth=8),
+             dict(x0=320, x_count=640, y0=100, row_count=200, max_depth=20),
+             dict(x0=0, x_count=320, y0=0, row_count=64, max_depth=8)]
+    for kw in cases:
+        job = gpu.Job(width=1280, height=720, frames=4, flags=512, **kw)
+        out = torch.zeros((kw["row_count"], kw["x_count"], 4), dtype=torch.float32, device="cuda")
+        rays = _torch_render(gpu, job, s, out)
+        info = L.last_launch()
+        assert info["kernel"] == "pool_kernel", info
+        s.synchronize()
+        want, wrays = oracle.orc_render(1280, 720, 4, kw["max_depth"], 0, kw["x0"], kw["x_count"], kw["y0"],
+                                        kw["row_count"], threads=16)
+        _bitwise(out.cpu().numpy(), want, f"window {kw}")
+        assert int(rays.item()) == wrays
+
+
+def test_kernel_timing_events(gpu):
+    """lrt_kernel_timing (lrt_diag.h): events right around each render kernel, read back in launch
+    order; off again, nothing more is recorded."""
+    import ctypes
+    import torch
+    from learnraytracing_amd import _lib as L
+    s = torch.cuda.current_stream()
+    job = gpu.Job(width=320, height=180, frames=4, max_depth=8)
+    out = torch.zeros((180, 320, 4), dtype=torch.float32, device="cuda")
+    L.check(L.lib().lrt_kernel_timing(1))
+    for _ in range(3):
+        _torch_render(gpu, job, s, out)
+    ms = (ctypes.c_float * 8)()
+    n = ctypes.c_int(-1)
+    L.check(L.lib().lrt_kernel_times(ms, 8, ctypes.byref(n)))
+    assert n.value == 3 and all(0.0 < ms[i] < 1000.0 for i in range(3)), (n.value, list(ms))
+    L.check(L.lib().lrt_kernel_timing(0))
+    _torch_render(gpu, job, s, out)
+    L.check(L.lib().lrt_kernel_times(ms, 8, ctypes.byref(n)))
+    assert n.value == 0
