@@ -151,8 +151,10 @@ __global__ __launch_bounds__(kBlock, kWavesPerEU) void trace_kernel(const Kernel
             for (int k = 0; k < 6; ++k)
                 fb[k] = (valid && a.feat[k]) ? a.feat[k][pix] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         }
+        // (a.lateFetch, few tasks per wave: the next task is reserved after this one's trace
+        // instead, so that the waves done first take the last tasks -- lrt_pool.h; profiles/r5_af)
         unsigned long long fetched = 0;
-        if (lane == 0) fetched = atomicAdd(ctr, 1ull);
+        if (!a.lateFetch && lane == 0) fetched = atomicAdd(ctr, 1ull);
         const int fbeg = kSamp ? a.frame0 + (task % rounds) * kSplit : a.frame0;
         const int fstop = kSamp ? fbeg + kSplit : fend;
         for (int f0 = fbeg; f0 < fstop; f0 += kSplit) {
@@ -211,6 +213,7 @@ __global__ __launch_bounds__(kBlock, kWavesPerEU) void trace_kernel(const Kernel
             }
             if (kSplit > 1) __builtin_amdgcn_wave_barrier();
         }
+        if (a.lateFetch && lane == 0) fetched = atomicAdd(ctr, 1ull);
         if (!kSamp && valid && sub == 0) {
             *px = acc;
             if (a.frame) a.frame[(size_t)y * a.width + x] = acc;   // the frame exchange, fused
@@ -312,6 +315,7 @@ int launch_depth(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     blocks = std::max(blocks, (long long)kV0Queues);
     if (blocks > tasks) blocks = tasks;
     const dim3 grid((unsigned)blocks);
+    a.lateFetch = tasks < 6LL * blocks * (kBlock / 64) ? 1 : 0;   // few tasks per wave: reserve late
     if (!a.sampOnly) a.samp = nullptr;
     a.ovf = nullptr;
     a.tiles = ctx().d_tiles + (size_t)(ctx().tiles_next++ % kQueueSlots) * kTileSetU64;
