@@ -408,6 +408,8 @@ def main():
     stream = torch.cuda.current_stream(dev)
     # render streams (the first is the current stream); frame assembly and D2H on their own
     rstreams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(nstreams - 1)]
+    for rs_ in rstreams[1:]:   # the buffers' zero fills (current stream) come before any render
+        rs_.wait_stream(stream)
     astream = torch.cuda.Stream(device=dev) if world > 1 else stream
     cstream = torch.cuda.Stream(device=dev)
     host = None   # pinned frame copies (end-to-end leg)

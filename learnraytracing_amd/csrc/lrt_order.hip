@@ -53,6 +53,7 @@ int order_used(Context::TileOrder& e, hipStream_t s) {
 int order_wait(Context::TileOrder& e, hipStream_t s) {
     if (!e.rec_done) {
         const hipError_t q = hipEventQuery(e.ev_rec);
+        (void)hipGetLastError();   // (a "not ready" answer must not look like the launch's error)
         if (q == hipSuccess) e.rec_done = true;
         else if (q != hipErrorNotReady) return hip_fail(q, "hipEventQuery(tile order)");
     }

@@ -88,7 +88,8 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     // waiting lanes that trigger a refill (fold + next samples). Measured (profiles/r2_p2):
     // config 3 2.31 -> 2.05 ms/step at 16 (vs 1), config 4 and config 2 neutral
     a.regenMin = 16;
-    // few tiles per wave (config 2: 14,400 tiles on 4,096 waves): reserve late (lrt_pool.h)
+    // few tiles per wave (config 2: 14,400 tiles on 4,096 waves): reserve late (lrt_pool.h;
+    // deciding by whether another stream's launch still runs was measured neutral, r5_ah)
     a.lateFetch = ntiles < 6LL * (long long)grid.x * wpb ? 1 : 0;
     a.poolSlots = kPix * std::min(a.frames, kPoolSamples / kPix);   // one round's samples
     const size_t nwaves = (size_t)grid.x * wpb;

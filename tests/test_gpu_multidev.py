@@ -208,6 +208,9 @@ def test_drawtest_pageable_buffer_freed_and_remapped_at_same_address(gpu):
 def _torch_render(gpu, job, stream, out):
     import torch
     rays = torch.zeros(1, dtype=torch.int64, device="cuda")
+    # `out` and `rays` were zero-filled on the current stream: the render on `stream` must come
+    # after those fills (without this a fill could land after the render's stores)
+    stream.wait_stream(torch.cuda.current_stream())
     gpu.render_tensor(job, out, rays, stream)
     return rays
 

@@ -342,6 +342,8 @@ def test_work_counters_across_slots_and_streams(gpu):
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
     bufs = [torch.zeros((180, 320, 4), dtype=torch.float32, device="cuda") for _ in range(8)]
     rays = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(8)]
+    for st in streams:   # after the buffers' zero fills (current stream)
+        st.wait_stream(torch.cuda.current_stream())
     for i in range(8):
         gpu.render_tensor(job, bufs[i], rays[i], streams[i % 2])
     torch.cuda.synchronize()
@@ -364,6 +366,7 @@ def test_cu_reserved_render_stream(gpu):
         try:
             buf = torch.zeros((180, 320, 4), dtype=torch.float32, device="cuda")
             rays = torch.zeros(1, dtype=torch.int64, device="cuda")
+            rs.torch.wait_stream(torch.cuda.current_stream())   # after the zero fills
             gpu.render_tensor(job, buf, rays, rs.torch)
             rs.torch.synchronize()
             assert int(rays.item()) == wr
