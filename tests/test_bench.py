@@ -52,3 +52,12 @@ def test_committed_pmc_summaries_are_consistent():
         assert abs(s["lane_ops_per_launch"] - c["SQ_INSTS_VALU"] * 64 * lu) <= 1e-6 * s["lane_ops_per_launch"]
         assert s["hbm_bytes_per_launch"] == 2 * c["FETCH_SIZE"] * 1024 + c["WRITE_SIZE"] * 1024
         assert s["kernel_trace"]["avg_ns"] > 0
+
+
+def test_default_steps_give_a_long_timed_region():
+    """Without --steps the timed region is tens of ms at every config (config 2: 200 steps of
+    ~0.22 ms; 20 steps measured the launch and drain edges at ~8 % of the region)."""
+    assert bench.DEFAULT_STEPS[2] == 200
+    approx_ms = {2: 0.22, 3: 1.8, 4: 84.0, 5: 1370.0}
+    for c, ms in approx_ms.items():
+        assert bench.DEFAULT_STEPS[c] * ms >= 40.0, c
