@@ -230,6 +230,8 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
     const int bq = (((int)gridDim.x - q + kV0Queues - 1) / kV0Queues) * kW;   // waves serving queue q
     const int nq = (ntiles - q + kV0Queues - 1) / kV0Queues;
     unsigned long long* ctr = a.tiles + q * kCtrStride;
+    // late tile reservation and issue priority by occupancy (below): the depth-8 one-wave instances
+    constexpr bool kLate = kW == 1 && MAXD <= 8;
     for (int i = (int)(blockIdx.x / kV0Queues) * kW + wave; i < nq;) {
         const int task = q + kV0Queues * i;
         const int tile = a.perm ? a.perm[task] : task;   // heaviest-first order (tile_order)
@@ -248,7 +250,6 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
         // (profiles/r5_z); with many tiles per wave the exposed latency costs more than the tail
         // (configs 3-4: +1-2 %, r5_n); only the depth-8 one-wave instances carry the code (its
         // presence alone cost config 3's instance 0.9 %, r5_aa).
-        constexpr bool kLate = kW == 1 && MAXD <= 8;
         unsigned long long fetched = 0;
         bool asked = !(kLate && a.lateFetch);
         if (asked && lane == 0) fetched = atomicAdd(ctr, 1ull);   // consumed after the tile
@@ -329,6 +330,13 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
                 if (traceM == 0) {
                     if (__ballot(state == kPoolIdle || state == kPoolEnded) == 0) break;   // the pool is dry
                     continue;
+                }
+                // A wave tracing few paths (its pool draining) yields the SIMD's issue slots to the
+                // fuller waves beside it: config 2 alone 0.2598 -> 0.2527 ms, two streams and
+                // configs 3-4 within noise (profiles/r5_al); the depth-8 one-wave instances only
+                if constexpr (kLate) {
+                    if (__popcll(traceM) < 24) __builtin_amdgcn_s_setprio(0);
+                    else __builtin_amdgcn_s_setprio(1);
                 }
                 // (no packet traversal here: without its code the instance keeps its traversal
                 // state in fewer registers, config 4: 222.4 -> 209.8 ms/step, profiles/r2_q2)
