@@ -200,3 +200,20 @@ def test_far_camera_window_vs_oracle(gpu, scene1000, kflags, cam_name):
     want, wr = oracle.orc_render(w, h, 16, 8, 0, 288, 64, 150, 40, spheres=s, mats=m, cam22=cam.to22(), threads=16)
     _bitwise(a, want, f"{cam_name} camera window")
     assert ra == wr
+
+
+@pytest.mark.parametrize("cam_name", sorted(FAR_CAMERAS))
+def test_far_camera_window_wavefront_vs_oracle(gpu, scene1000, cam_name):
+    """The same far cameras through the v4 wavefront kernels (LRT_F_WAVEFRONT), whose extend
+    kernel traces the BVH: its per-ray excursion margins hold there too."""
+    s, m = scene1000
+    frm, at, vfov = FAR_CAMERAS[cam_name]
+    w, h = 640, 360
+    dist = float(np.linalg.norm(np.subtract(frm, at)))
+    cam = gpu.make_camera(frm, at, (0, 1, 0), vfov, w / h, 0.1, dist)
+    kw = dict(width=w, height=h, frames=4, max_depth=8, x0=288, x_count=64, y0=150, row_count=40, camera=cam)
+    a, ra, info = _render(gpu, flags=256, **kw)
+    assert info["kernel"] == "wf_extend" and info["bvh"] == "1", info
+    want, wr = oracle.orc_render(w, h, 4, 8, 0, 288, 64, 150, 40, spheres=s, mats=m, cam22=cam.to22(), threads=16)
+    _bitwise(a, want, f"{cam_name} camera window (wavefront)")
+    assert ra == wr
