@@ -13,13 +13,13 @@
 #   ab=V,C[,ARGS]     bench.py --config C with LRT_LIB=build_exp/liblrt_V.so (tools/build_variant.sh),
 #                     timed region only (A/B of library variants; V=default: the in-tree library;
 #                     NAME=VALUE tokens in ARGS set environment variables)
-# Output: gpurun_out/$TAG/<step>.log (+ rocprof CSVs).
+# Output: gpurun_out/$TAG/<step>.log (+ rocprof CSVs). BSTEPS: timed steps (default: bench.py's per-config default).
 cd "$GRAFT_REPO_ROOT" || exit 1
 TAG=${TAG:-latest}
 out=gpurun_out/$TAG
 mkdir -p "$out"
 export TMPDIR=/tmp
-BSTEPS=${BSTEPS:-20}
+BSTEPS=${BSTEPS:-default}
 STEPARG=(--steps "$BSTEPS")
 [ "$BSTEPS" = default ] && STEPARG=()   # bench.py's per-config default
 declare -A PMC=(
