@@ -264,6 +264,76 @@ def read_pmc(key: str):
         return None
 
 
+def base_line(args, world, cfg):
+    """The fields every line carries, the failure lines included (value null)."""
+    return {"metric": METRIC, "value": None, "unit": "Mray/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
+            "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"config{args.config}: {cfg['width']}x{cfg['height']}, "
+                                   f"{cfg['spp_total']} spp, {cfg['depth']} bounces"}}
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(args, argv) -> int:
+    """`--gpus N` (N > 1) without a launcher: start N ranks as ONE child process,
+    `python -m torch.distributed.run --nproc-per-node N ... bench.py <same args>`, forward rank
+    0's JSON line and return the child's exit code. This process never imports torch or touches
+    a GPU (the child is started, not exec'd). If the child cannot start, or ends without a line,
+    print a line with value null naming the reason and return non-zero: a run asked for N GPUs
+    never reports a one-GPU number."""
+    import collections
+    import subprocess
+
+    n = args.gpus
+    base = base_line(args, n, workload(args.config, n, args.scaling, args.spp, args.depth))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    log(f"bench: --gpus {n} without a launcher: starting {n} ranks: {' '.join(cmd)}")
+
+    def fail(reason, rc):
+        line = dict(base)
+        line.update({"error": reason, "launcher": "bench.py self-launch (torch.distributed.run)"})
+        print(json.dumps(line), flush=True)
+        return rc if rc else 1
+
+    try:
+        p = subprocess.Popen(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, bufsize=1)
+    except OSError as e:
+        return fail(f"could not start torch.distributed.run: {e}", 2)
+    tail = collections.deque(maxlen=30)
+
+    def pump_err():
+        for ln in p.stderr:
+            tail.append(ln.rstrip())
+            sys.stderr.write(ln)
+            sys.stderr.flush()
+
+    t = threading.Thread(target=pump_err, daemon=True)
+    t.start()
+    lines = 0
+    for ln in p.stdout:
+        if ln.startswith("{"):
+            lines += 1
+            sys.stdout.write(ln)
+            sys.stdout.flush()
+        else:
+            sys.stderr.write(ln)
+    rc = p.wait()
+    t.join(timeout=5)
+    if lines == 0:
+        return fail(f"the {n}-rank run exited with status {rc} without a result line; stderr tail: "
+                    + " | ".join(list(tail)[-8:]), rc)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -300,19 +370,24 @@ def main():
     if args.steps is None:
         args.steps = DEFAULT_STEPS.get(args.config, 20)
 
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(self_launch(args, sys.argv[1:]))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: WORLD_SIZE={world} but --gpus {args.gpus}; using WORLD_SIZE")
     cfg = workload(args.config, world, args.scaling, args.spp, args.depth, args.shard_of)
     cfg_name = f"config{args.config}"
+    if world != args.gpus:   # a launcher's rank count and --gpus disagree: refuse, never relabel
+        if rank == 0:
+            line = base_line(args, args.gpus, cfg)
+            line["error"] = f"WORLD_SIZE={world} but --gpus {args.gpus}: the launcher and --gpus disagree"
+            print(json.dumps(line), flush=True)
+        log(f"error: WORLD_SIZE={world} but --gpus {args.gpus}")
+        sys.exit(2)
     extra = not args.no_extra_legs
-    wd = Watchdog(rank, world, {
-        "metric": METRIC, "value": None, "unit": "Mray/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
-        "dtype": "f32", "data": "synthetic", "config": {"workload": f"{cfg_name}: {cfg['width']}x{cfg['height']}, "
-                                                                    f"{cfg['spp_total']} spp, {cfg['depth']} bounces"}})
+    wd = Watchdog(rank, world, base_line(args, world, cfg))
 
     # CPU baselines first: rank 0 at N=1 only, before anything touches the GPU.
     cpu = cpu1 = cpu_dt = None
@@ -338,15 +413,32 @@ def main():
     backend = os.environ.get("LRT_DIST_BACKEND", "nccl")   # nccl = RCCL; gloo only to rehearse on 1 GPU
     # LRT_BENCH_SAME_GPU=1 puts every rank on GPU 0 (rehearsing the RCCL path on a 1-GPU box)
     gpu = 0 if (backend != "nccl" or os.environ.get("LRT_BENCH_SAME_GPU") == "1") else local_rank
+    def check_devices():
+        """Refuse a world the visible GPUs cannot hold (one rank per GPU over RCCL), rank 0
+        printing the line -- never fewer GPUs than the line's n_gpus. (Counting devices does
+        not initialise the GPU.)"""
+        ndev = torch.cuda.device_count()
+        if gpu < ndev and not (backend == "nccl" and gpu == local_rank and world > ndev):
+            return
+        msg = f"--gpus {world} needs {world if gpu == local_rank else 1} visible GPU(s), {ndev} visible"
+        if rank == 0:
+            line = dict(wd.base)
+            line.update({"error": msg, "failed_phase": "device_count"})
+            print(json.dumps(line), flush=True)
+        log(f"rank {rank}: error: {msg}")
+        os._exit(2)
+
     if world > 1:   # the rendezvous itself is bounded too (the store's timeout)
         wd.enter("init_process_group")
         tmo = datetime.timedelta(seconds=wd.limit * 1.5)   # (the watchdog reports first)
         if backend == "nccl":
+            check_devices()
             torch.cuda.set_device(gpu)
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu), timeout=tmo)
         else:
             dist.init_process_group(backend, timeout=tmo)
     wd.enter("device_init", max(wd.limit, 300.0))
+    check_devices()
     torch.cuda.set_device(gpu)
     import learnraytracing_amd as lrt
     from learnraytracing_amd import _lib as L

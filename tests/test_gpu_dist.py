@@ -240,3 +240,20 @@ def test_fused_frame_store_every_kernel(gpu, kernel, scene):
         if scene == "scene1000":
             gpu.set_scene(*gpu.default_scene())
     assert np.array_equal(got[..., :3].view(np.uint32), want[..., :3].view(np.uint32)), kernel
+
+
+def test_bench_gpus_2_self_launches(gpu):
+    """`python bench.py --gpus 2` with no launcher around it (the shape of the driver's
+    command) starts its two ranks itself and reports both: n_gpus 2 and config 2's own ray
+    count (round-5 verdict, Next 1). Both ranks share GPU 0 (gloo control plane)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["LRT_DIST_BACKEND"] = "gloo"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--no-cpu-baseline"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["rays_per_step"] == 11669343, d
+    assert d["exchange"]["frames_identical"] is True, d["exchange"]
