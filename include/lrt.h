@@ -99,9 +99,6 @@ typedef struct lrt_render_desc {
 #define LRT_F_SIMPLE 2       /* v0 kernel (the default): the reference's per-pixel loop,
                                 a pixel's frames spread over adjacent lanes, persistent
                                 single-wave blocks fed from tile queues               */
-#define LRT_F_V1 4           /* removed (round-1 per-lane state machine, always slower
-                                than SIMPLE): rejected with LRT_E_INVALID             */
-#define LRT_F_V2S 8          /* removed, as LRT_F_V1                                   */
 #define LRT_F_NO_BVH 32      /* scan every sphere (the reference's HitWorld loop) even
                                 when the scene has a BVH (> 16 spheres)                */
 #define LRT_F_NO_DOUBLE_LIGHT 64 /* opt-in GL-path rule (fragmentShader.fs.glsl:430,456-457,
@@ -110,10 +107,6 @@ typedef struct lrt_render_desc {
                                 sampled explicitly); the terminating hit always adds it.
                                 Off by default: the CPU reference double counts
                                 (parallel.cpp:214). v0 kernel only.                   */
-#define LRT_F_V2 16          /* removed, as LRT_F_V1. With none of SIMPLE/WAVEFRONT/POOL
-                                set the library picks v0 or v5 per call (auto_kernel). */
-#define LRT_F_V3 128         /* removed in round 3 (round-1 path regeneration per pixel
-                                group: slower than v0 or v5 on every config), as LRT_F_V1 */
 #define LRT_F_WAVEFRONT 256  /* v4: wavefront (breadth-first) path tracing: path state in
                                 HBM, closest-hit and per-material shading kernels over
                                 compacted queues, frame planes merged in order. No
@@ -127,6 +120,9 @@ typedef struct lrt_render_desc {
                                 would pick the uniform grid (scenes above 16 spheres) */
 #define LRT_F_GRID 2048      /* closest hits through the uniform grid (lrt_grid.h) even where
                                 the library would pick the BVH; same bits either way */
+/* With none of SIMPLE / WAVEFRONT / POOL set the library picks v0 or v5 per call. Any bit not
+ * defined above (4, 8, 16 and 128 belonged to kernels removed in rounds 2-3) is rejected with
+ * LRT_E_INVALID. */
 
 /* ---- the reference API (parallel.h:6-8) ---------------------------------- */
 
@@ -199,7 +195,9 @@ int lrt_default_scene(lrt_sphere* spheres, lrt_material* materials, int capacity
 
 /* Render into a DEVICE buffer of row_count * x_count RGBA float quads (row-major,
  * local rows), adding the counted rays into *d_rays (device uint64, caller-zeroed).
- * Asynchronous on `stream` (a hipStream_t, used as given: NULL is the default stream). */
+ * Asynchronous on `stream` (a hipStream_t, used as given: NULL is the default stream), and
+ * ordered only against that stream: a buffer or counter filled on another stream must be
+ * ordered before the call by the caller (an event, or a stream wait). */
 int lrt_render_device(const lrt_render_desc* desc, float* d_backbuffer,
                       unsigned long long* d_rays, void* stream);
 
@@ -272,9 +270,7 @@ int lrt_host_free(void* p);
  * starts, hipHostUnregister before it returns) and takes the page-locked paths. The library
  * keeps nothing of the caller's buffer between calls: the caller may free it, or reuse or
  * remap its address, at any time between calls -- DrawTest's own contract (parallel.h:8).
- * LRT_HOST_REGISTER=0 stages pageable buffers instead. lrt_host_unregister is a no-op kept
- * for callers of the round-3 API (returns LRT_OK). */
-int lrt_host_unregister(void* p);
+ * LRT_HOST_REGISTER=0 stages pageable buffers instead. */
 
 /* Number of local rows GPU `phase` owns in a row-block-cyclic split of `height` rows
  * into blocks of row_block rows dealt over `period` GPUs. */

@@ -8,7 +8,7 @@ liblrt_hip.so only (no CPU fallback).
 """
 from ._lib import LrtError, lib  # noqa: F401
 from .renderer import (DrawTest, InitializeDevices, InitializeTest, Job, ShutdownTest,  # noqa: F401
-                       default_camera, device_count, host_unregister, make_camera, pinned_backbuffer,
+                       default_camera, device_count, make_camera, pinned_backbuffer,
                        get_scene, render_device, render_host, render_host_features, render_tensor,
                        render_tensor_to_frame, set_scene, shard_rows)
 from .scene import default_scene, random_scene  # noqa: F401

@@ -27,14 +27,13 @@ REFERENCE_MAX_DEPTH = 20                      # parallel.cpp:12
 MAX_SPHERES = 4096
 F_SCENE_GLOBAL = 1
 F_SIMPLE = 2
-F_V1 = 4            # removed kernels: rejected with LRT_E_INVALID
-F_V2S = 8
-F_V2 = 16
 F_NO_BVH = 32
 F_NO_DOUBLE_LIGHT = 64
-F_V3 = 128          # removed in round 3: rejected with LRT_E_INVALID
 F_WAVEFRONT = 256
 F_POOL = 512
+F_BVH = 1024
+F_GRID = 2048
+REMOVED_FLAG_BITS = (4, 8, 16, 128)   # v1, v2s, v2, v3 (rounds 2-3): rejected with LRT_E_INVALID
 DEV_PEER_COPY = 1   # lrt_initialize_devices: gather by device-to-device copies, not RCCL
 DEV_GATHER = 2      # lrt_initialize_devices: gather the shards into the first device (RCCL)
 IPC_HANDLE_BYTES = 64
@@ -96,7 +95,7 @@ FEATURE_NAMES = ("normal", "world_pos", "albedo", "color_std", "normal_std", "wo
 _c = ctypes
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
-# name -> (restype, argtypes); must cover every function include/lrt.h declares
+# name -> (restype, argtypes); must cover every function include/lrt.h declares (required)
 SIGNATURES = {
     "lrt_initialize": (_i, []),
     "lrt_shutdown": (_i, []),
@@ -105,7 +104,6 @@ SIGNATURES = {
     "lrt_version": (_c.c_char_p, []),
     "lrt_initialize_devices": (_i, [_i, _vp, _i]),
     "lrt_device_count": (_i, []),
-    "lrt_host_unregister": (_i, [_vp]),
     "lrt_last_launch": (_c.c_char_p, []),
     "lrt_camera_make": (_i, [Float3, Float3, Float3, _c.c_float, _c.c_float, _c.c_float,
                              _c.c_float, _c.POINTER(Camera)]),
@@ -132,6 +130,10 @@ SIGNATURES = {
     "lrt_pack_rgb": (_i, [_vp, _vp, _c.c_longlong, _vp]),
     "lrt_unshard_rows_rgb": (_i, [_vp, _vp, _i, _i, _i, _i, _vp]),
     "lrt_present_bgra8": (_i, [_vp, _vp, _i, _i, _vp]),
+}
+# include/lrt_diag.h: diagnostics and test hooks, bound when the library exports them (the
+# product path needs none of them; a build without them still loads)
+DIAG_SIGNATURES = {
     "lrt_libm_eval_host": (_i, [_i, _vp, _vp, _c.c_longlong]),
     "lrt_libm_eval_device": (_i, [_i, _vp, _vp, _c.c_longlong]),
     "lrt_bvh_stats": (_i, [_c.POINTER(Sphere), _i, _vp, _i, _vp]),
@@ -168,9 +170,9 @@ def lib() -> ctypes.CDLL:
                 handle = ctypes.CDLL(LIB_PATH)
             except OSError as e:   # pragma: no cover - depends on the box
                 raise LrtError(LRT_E_STATE, f"cannot load {LIB_PATH}: {e}") from e
-            for name, (res, args) in SIGNATURES.items():
+            for name, (res, args) in list(SIGNATURES.items()) + list(DIAG_SIGNATURES.items()):
                 fn = getattr(handle, name, None)
-                if fn is None and os.environ.get("LRT_LIB"):
+                if fn is None and (name in DIAG_SIGNATURES or os.environ.get("LRT_LIB")):
                     continue   # an A/B build of an older revision: entry points it predates stay unbound
                 if fn is None:
                     raise LrtError(LRT_E_STATE, f"{LIB_PATH} does not export {name}")

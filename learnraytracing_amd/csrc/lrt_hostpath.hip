@@ -381,14 +381,3 @@ int render_host(const lrt_render_desc* d, float* buf, long long* out_rays, const
 }
 
 }  // namespace lrt
-
-using namespace lrt;
-
-extern "C" {
-
-int lrt_host_unregister(void* p) {
-    (void)p;   // nothing to undo: a pageable buffer is page-locked only within a call (HostLock)
-    return LRT_OK;
-}
-
-}  // extern "C"

@@ -24,7 +24,12 @@
 
 namespace lrt {
 
-enum : int { kPoolIdle = 0, kPoolTrace = 1, kPoolDone = 2, kPoolEnded = 3 };
+enum : int { kPoolIdle = 0, kPoolTrace = 1, kPoolDone = 2, kPoolEnded = 3, kPoolRare = 4 };
+
+// Metal / Dielectric scatter deferral (A/B, LRT_POOL_DEFER=K lanes; 0 = off): see pool_kernel.
+#ifndef LRT_POOL_DEFER
+#define LRT_POOL_DEFER 0
+#endif
 
 template <int kPix>
 struct PoolTile {   // tile shape: kPix pixels, as square as a power of two allows
@@ -232,6 +237,7 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
     unsigned long long* ctr = a.tiles + q * kCtrStride;
     // late tile reservation and issue priority by occupancy (below): the depth-8 one-wave instances
     constexpr bool kLate = kW == 1 && MAXD <= 8;
+    constexpr int kDefer = kLate ? LRT_POOL_DEFER : 0;
     for (int i = (int)(blockIdx.x / kV0Queues) * kW + wave; i < nq;) {
         const int task = q + kV0Queues * i;
         const int tile = a.perm ? a.perm[task] : task;   // heaviest-first order (tile_order)
@@ -327,7 +333,7 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
                     }
                 }
                 const unsigned long long traceM = __ballot(state == kPoolTrace);
-                if (traceM == 0) {
+                if (traceM == 0 && (!kDefer || __ballot(state == kPoolRare) == 0)) {
                     if (__ballot(state == kPoolIdle || state == kPoolEnded) == 0) break;   // the pool is dry
                     continue;
                 }
@@ -343,12 +349,14 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
                 constexpr bool coherent = false;
                 sec_enter(sc, kSecOther, false);
                 // ---- one bounce of every traced path: Trace's body (parallel.cpp:202-226) ----
+                int nid = -1;
+                float nt = 0.0f;
+                bool shade = false, fin = false;
+                F3 leaf = f3(0.0f, 0.0f, 0.0f);
                 if (state == kPoolTrace) {
                     // HitWorld of r (:204-205) and the pending shadow ray (:122-123) in one pass
                     sec_count(sc, coherent ? kSecHit0 : kSecHit);
                     ++rays;
-                    int nid;
-                    float nt;
                     bool lit = false;
                     const bool hasS = pend && dl.on;
                     if constexpr (kAcc == kAccGrid) {
@@ -373,47 +381,69 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
                         ++depth;
                         pend = false;
                     }
-                    F3 leaf;
-                    bool fin = false;
                     if (nid < 0) {   // sky (:223-225)
                         const float t = 0.5f * (r.dir.y + 1.0f);
                         leaf = ((1.0f - t) * f3(1.0f, 1.0f, 1.0f) + t * f3(0.5f, 0.7f, 1.0f)) * 0.3f;
                         fin = true;
-                    } else {   // HitWorld's winner (maths.cpp:74-76,86-88), then Scatter (:210-212)
-                        const float4 sp4 = sc.sph[nid];
-                        Hit rec;
-                        rec.pos = point_at(r, nt);
-                        rec.normal = normalize(rec.pos - f3(sp4.x, sp4.y, sp4.z));
-                        rec.t = nt;
-                        const Material mat = load_material(sc.mats, nid);
-                        F3 matE = mat.emissive;
-                        fin = true;
-                        leaf = matE;
-                        if (depth < a.maxDepth) {
-                            F3 lightE;
-                            dl.on = false;
-                            if constexpr (kAcc == kAccGrid) sc.gv = pool_grid_view<kAcc, kW>(smem);   // other lights' shadow rays
-                            const F3 X = ScatterDir<kAcc, kNS>(mat, nid, r, rec, lightE, rays, rng, sc, &dl, coherent);
-                            sec_count(sc, kSecPost);
-                            const F3 dir = renormalize(normalize(X), sc.rnlut);   // Ray(rec.pos, normalize(X))
-                            if ((mat.type != 1) | (dot(dir, rec.normal) > 0.0f)) {    // Metal absorbs (:147)
-                                if (a.ndl && prevLambert) matE = f3(0.0f, 0.0f, 0.0f);
-                                prevLambert = mat.type == 0;
-                                const F3 e = matE + lightE;
-                                put(depth, make_float4(e.x, e.y, e.z, __int_as_float(nid)));
-                                if (dl.on) carry = matE + (lightE + dl.contrib);   // TraceDual's order
-                                dl.id = nid;
-                                pend = true;
-                                r.orig = rec.pos;
-                                r.dir = dir;
-                                fin = false;
-                            }
+                    } else if (kDefer && depth < a.maxDepth && __float_as_int(sc.mats[3 * nid].w) != 0) {
+                        // a Metal or Dielectric hit parks the path until enough lanes hold one (below):
+                        // its hit (nid, nt) waits in registers the path does not use until it scatters
+                        // (the pending light's, already consumed above)
+                        state = kPoolRare;
+                        dl.li = nid;
+                        carry.x = nt;
+                    } else {
+                        shade = true;
+                    }
+                }
+                if constexpr (kDefer) {
+                    // Parked paths scatter together once kDefer of them wait, or when no path is left
+                    // to trace: the Metal / Dielectric regions then run with more lanes (profiles/r6_*).
+                    // Each path's events keep their order and its RNG stream is its own: same bits.
+                    const unsigned long long rareM = __ballot(state == kPoolRare);
+                    if (rareM && (__popcll(rareM) >= kDefer || __ballot(shade) == 0)) {
+                        if (state == kPoolRare) {
+                            nid = dl.li;
+                            nt = carry.x;
+                            shade = true;
+                            state = kPoolTrace;
                         }
                     }
-                    if (fin) {   // the path's leaf colour waits for the fold at the next refill
-                        carry = leaf;
-                        state = kPoolEnded;
+                }
+                if (shade) {   // HitWorld's winner (maths.cpp:74-76,86-88), then Scatter (:210-212)
+                    const float4 sp4 = sc.sph[nid];
+                    Hit rec;
+                    rec.pos = point_at(r, nt);
+                    rec.normal = normalize(rec.pos - f3(sp4.x, sp4.y, sp4.z));
+                    rec.t = nt;
+                    const Material mat = load_material(sc.mats, nid);
+                    F3 matE = mat.emissive;
+                    fin = true;
+                    leaf = matE;
+                    if (depth < a.maxDepth) {
+                        F3 lightE;
+                        dl.on = false;
+                        if constexpr (kAcc == kAccGrid) sc.gv = pool_grid_view<kAcc, kW>(smem);   // other lights' shadow rays
+                        const F3 X = ScatterDir<kAcc, kNS>(mat, nid, r, rec, lightE, rays, rng, sc, &dl, coherent);
+                        sec_count(sc, kSecPost);
+                        const F3 dir = renormalize(normalize(X), sc.rnlut);   // Ray(rec.pos, normalize(X))
+                        if ((mat.type != 1) | (dot(dir, rec.normal) > 0.0f)) {    // Metal absorbs (:147)
+                            if (a.ndl && prevLambert) matE = f3(0.0f, 0.0f, 0.0f);
+                            prevLambert = mat.type == 0;
+                            const F3 e = matE + lightE;
+                            put(depth, make_float4(e.x, e.y, e.z, __int_as_float(nid)));
+                            if (dl.on) carry = matE + (lightE + dl.contrib);   // TraceDual's order
+                            dl.id = nid;
+                            pend = true;
+                            r.orig = rec.pos;
+                            r.dir = dir;
+                            fin = false;
+                        }
                     }
+                }
+                if (fin) {   // the path's leaf colour waits for the fold at the next refill
+                    carry = leaf;
+                    state = kPoolEnded;
                 }
             }
             // ---- the round's colours in frame order, one lane per pixel (:262,282) ---------

@@ -307,8 +307,10 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     if (rc) return rc;
     if (!ctx().ready) return fail(LRT_E_STATE, "lrt_initialize() has not been called");
     if (!d_buf || !d_rays) return fail(LRT_E_INVALID, "device buffer / ray counter is NULL");
-    if (d->flags & (LRT_F_V1 | LRT_F_V2S | LRT_F_V2 | LRT_F_V3))   // (every path, the colours-only one too)
-        return fail(LRT_E_INVALID, "LRT_F_V1/LRT_F_V2S/LRT_F_V2/LRT_F_V3 kernels were removed (the default picks v0 or v5)");
+    constexpr int kKnownFlags = LRT_F_SCENE_GLOBAL | LRT_F_SIMPLE | LRT_F_NO_BVH | LRT_F_NO_DOUBLE_LIGHT |
+                                LRT_F_WAVEFRONT | LRT_F_POOL | LRT_F_BVH | LRT_F_GRID;
+    if (d->flags & ~kKnownFlags)   // (every path, the colours-only one too; 4/8/16/128: removed kernels)
+        return fail(LRT_E_INVALID, "unknown LRT_F_* flag (the v1/v2/v3 kernels were removed: the default picks v0 or v5)");
     if (d->x_count == 0 || d->row_count == 0 || d->frames == 0) return LRT_OK;
     KernelArgs a;
     const lrt_camera& c = d->camera;

@@ -53,12 +53,6 @@ def device_count() -> int:
     return int(L.lib().lrt_device_count())
 
 
-def host_unregister(backbuffer: np.ndarray) -> None:
-    """No-op kept for callers of round 3's API: the library page-locks a pageable buffer only
-    for the duration of one call and keeps no registration between calls."""
-    L.check(L.lib().lrt_host_unregister(backbuffer.ctypes.data_as(ctypes.c_void_p)))
-
-
 def DrawTest(time: float, frameCount: int, screenWidth: int, screenHeight: int,
              backbuffer: np.ndarray) -> int:
     """The reference's DrawTest (parallel.h:8): one progressive frame into the caller's

@@ -37,7 +37,16 @@ def test_library_exports_every_declared_symbol():
     lib = L.lib()
     for n in api + diag:
         assert hasattr(lib, n), n
-    assert set(api + diag) == set(L.SIGNATURES), "ctypes signatures out of sync with include/lrt.h + lrt_diag.h"
+    assert set(api) == set(L.SIGNATURES), "ctypes signatures out of sync with include/lrt.h"
+    assert set(diag) == set(L.DIAG_SIGNATURES), "ctypes signatures out of sync with include/lrt_diag.h"
+
+
+def test_removed_entry_points_and_flags_are_gone():
+    """Round 6 trimmed the surface: no no-op lrt_host_unregister, no removed-kernel flags."""
+    src = open(L.HEADER_PATH).read()
+    for name in ("LRT_F_V1", "LRT_F_V2S", "LRT_F_V2 ", "LRT_F_V3", "lrt_host_unregister"):
+        assert name not in src, name
+    assert "lrt_host_unregister" not in exported_functions()
 
 
 def test_exported_symbol_set_is_the_two_headers():

@@ -103,6 +103,6 @@ def test_modes_need_v0(gpu):
         gpu.render_host_features(_job(gpu, 64, 36, 2, 8, flags=L.F_POOL), buf, {"normal": buf.copy()})
     with pytest.raises(LrtError):
         gpu.render_host_features(_job(gpu, 64, 36, 2, 8, flags=L.F_WAVEFRONT), buf, {"normal": buf.copy()})
-    for removed in (L.F_V1, L.F_V2S, L.F_V2, L.F_V3):   # removed kernels: rejected loudly
+    for removed in L.REMOVED_FLAG_BITS:   # removed kernels: rejected loudly
         with pytest.raises(LrtError):
             gpu.render_host(_job(gpu, 64, 36, 2, 8, flags=removed), buf)

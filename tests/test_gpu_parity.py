@@ -390,11 +390,13 @@ def test_kernel_config2_full_frame_vs_oracle(gpu, kflags):
     assert rays == wrays
 
 
-def test_v3_flag_is_rejected(gpu):
-    """Round 3 removed v3 (LRT_F_V3): the flag fails loudly instead of running another kernel."""
+@pytest.mark.parametrize("bit", [4, 8, 16, 128, 1 << 20])
+def test_removed_and_unknown_flags_are_rejected(gpu, bit):
+    """The removed kernels' bits (v1 4, v2s 8, v2 16, v3 128) and any other undefined bit fail
+    loudly instead of running another kernel."""
     from learnraytracing_amd import _lib as L
     with pytest.raises(L.LrtError) as e:
-        _render(gpu, 16, 8, 1, 8, flags=L.F_V3)
+        _render(gpu, 16, 8, 1, 8, flags=bit)
     assert e.value.code == L.LRT_E_INVALID
 
 
