@@ -84,8 +84,10 @@ void free_context(Context& c) {
         if (f) (void)hipFree(f);
     for (auto& m : c.masked_streams) (void)hipStreamDestroy(m.first);
     if (c.d_col) (void)hipFree(c.d_col);
-    for (auto& sc : c.scratch)
+    for (auto& sc : c.scratch) {
         if (sc.p) (void)hipFree(sc.p);
+        if (sc.ev) (void)hipEventDestroy(sc.ev);
+    }
     for (auto& o : c.order) {
         if (o.d_base) (void)hipFree(o.d_base);
         if (o.ev_rec) (void)hipEventDestroy(o.ev_rec);

@@ -182,13 +182,17 @@ struct Context {
     // Per-stream scratch of the pool kernel (colour slots, overflow stack), kept from launch to
     // launch: an allocation and a free around every launch put two more commands between
     // consecutive kernels of a stream (profiles/r5_s). Reuse on the same stream is ordered by the
-    // stream itself; a buffer grows by a stream-ordered free + allocation on that stream.
+    // stream itself; a buffer grows by a stream-ordered free + allocation on that stream. `ev` is
+    // recorded behind the buffer's last use: a slot taken over by another stream (or idle for
+    // kScratchIdle launches) is freed on the taking stream after waiting for it -- no device sync.
     struct Scratch {
         hipStream_t s = nullptr;
         void* p = nullptr;
         size_t bytes = 0;
         unsigned long long tick = 0;
+        hipEvent_t ev = nullptr;
     };
+    static constexpr unsigned long long kScratchIdle = 64;
     static constexpr int kScratchSlots = 8;
     Scratch scratch[kScratchSlots];
     static constexpr int kOrderSlots = 8;
@@ -346,7 +350,13 @@ int camera_default(int w, int h, lrt_camera* out);
 // ---- lrt_render.hip
 int validate(const lrt_render_desc* d);
 // At least `bytes` of device scratch for launches on stream s (Context::scratch).
+// Has ev completed? An error left pending by an earlier asynchronous call is returned first (not
+// cleared); only the "not ready" the query itself sets is cleared, so that it does not look like
+// a later launch's error.
+hipError_t event_done(hipEvent_t ev, bool* done);
 hipError_t stream_scratch(hipStream_t s, size_t bytes, void** out);
+// After the launch that used stream s's scratch: marks its last use (stream_scratch eviction).
+hipError_t stream_scratch_used(hipStream_t s);
 // lrt_kernel_timing (lrt_diag.h): events right around each render kernel launch on its stream
 extern bool g_ktiming_on;
 void kernel_timing_mark(hipStream_t s, int which);   // 0 before the kernel, 1 after

@@ -52,10 +52,9 @@ int order_used(Context::TileOrder& e, hipStream_t s) {
 // which no launch needs the wait (one command fewer between a stream's kernels).
 int order_wait(Context::TileOrder& e, hipStream_t s) {
     if (!e.rec_done) {
-        const hipError_t q = hipEventQuery(e.ev_rec);
-        (void)hipGetLastError();   // (a "not ready" answer must not look like the launch's error)
-        if (q == hipSuccess) e.rec_done = true;
-        else if (q != hipErrorNotReady) return hip_fail(q, "hipEventQuery(tile order)");
+        bool done = false;
+        if (const hipError_t q = event_done(e.ev_rec, &done)) return hip_fail(q, "hipEventQuery(tile order)");
+        e.rec_done = done;
     }
     if (!e.rec_done) LRT_HIP(hipStreamWaitEvent(s, e.ev_rec, 0));
     return LRT_OK;

@@ -152,6 +152,8 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
         if (record) users[0]->state = 0;   // nothing recorded: the entry is free again
         return hip_fail(e, "pool_kernel launch");
     }
+    e = stream_scratch_used(s);
+    if (e != hipSuccess) return hip_fail(e, "pool scratch event");
     if (record) {   // the costs just recorded, sorted on the device behind the launch
         Context::TileOrder& o = *users[0];
         e = sort_tiles_desc(o.d_cost, o.d_keys, o.d_ids, o.d_sort_out, (int)ntiles, o.d_tmp, &o.tmp_bytes, s);

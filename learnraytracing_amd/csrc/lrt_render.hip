@@ -120,23 +120,56 @@ void secstats_dump(const unsigned long long* d_sec, hipStream_t s) {
 #endif
 
 
+hipError_t event_done(hipEvent_t ev, bool* done) {
+    *done = false;
+    const hipError_t pending = hipGetLastError();
+    if (pending != hipSuccess) return pending;
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) {
+        *done = true;
+        return hipSuccess;
+    }
+    if (q != hipErrorNotReady) return q;
+    (void)hipGetLastError();   // the query's own "not ready"
+    return hipSuccess;
+}
+
+// Release slot e's buffer from stream s: s waits for the buffer's last use (its event), then
+// frees it in stream order. The owning stream may be gone; its recorded event still completes.
+static hipError_t scratch_release(Context::Scratch& e, hipStream_t s) {
+    hipError_t r = hipSuccess;
+    if (e.p) {
+        r = hipStreamWaitEvent(s, e.ev, 0);
+        if (r == hipSuccess) r = hipFreeAsync(e.p, s);
+    }
+    e.p = nullptr;
+    e.bytes = 0;
+    e.s = nullptr;
+    return r;
+}
+
 hipError_t stream_scratch(hipStream_t s, size_t bytes, void** out) {
     Context& c = ctx();
     Context::Scratch* hit = nullptr;
     for (auto& e : c.scratch)
         if (e.p && e.s == s) hit = &e;
-    if (!hit) {   // a free slot, or the least recently used one (its stream may be gone: a full sync)
+    const unsigned long long now = ++c.order_tick;
+    for (auto& e : c.scratch)   // buffers of streams idle for kScratchIdle launches, seen done: released
+        if (e.p && &e != hit && now - e.tick > Context::kScratchIdle) {
+            bool done = false;
+            if (const hipError_t r = event_done(e.ev, &done)) return r;
+            if (done)
+                if (const hipError_t r = scratch_release(e, s)) return r;
+        }
+    if (!hit) {   // a free slot, or the least recently used one (taken over in stream order)
         hit = &c.scratch[0];
         for (auto& e : c.scratch)
             if (!e.p || (hit->p && e.tick < hit->tick)) hit = &e;
-        if (hit->p) {
-            hipError_t e = hipDeviceSynchronize();
-            if (e == hipSuccess) e = hipFree(hit->p);
-            if (e != hipSuccess) return e;
-        }
-        *hit = Context::Scratch();
+        if (const hipError_t r = scratch_release(*hit, s)) return r;
         hit->s = s;
     }
+    if (!hit->ev)
+        if (const hipError_t r = hipEventCreateWithFlags(&hit->ev, hipEventDisableTiming)) return r;
     if (hit->bytes < bytes) {   // grow, ordered on the stream that uses it
         if (hit->p) {
             const hipError_t e = hipFreeAsync(hit->p, s);
@@ -150,9 +183,17 @@ hipError_t stream_scratch(hipStream_t s, size_t bytes, void** out) {
             return e;
         }
         hit->bytes = bytes;
+        // (the allocation is the buffer's first use until a launch records over it)
+        if (const hipError_t r = hipEventRecord(hit->ev, s)) return r;
     }
-    hit->tick = ++c.order_tick;
+    hit->tick = now;
     *out = hit->p;
+    return hipSuccess;
+}
+
+hipError_t stream_scratch_used(hipStream_t s) {
+    for (auto& e : ctx().scratch)
+        if (e.p && e.s == s) return hipEventRecord(e.ev, s);
     return hipSuccess;
 }
 

@@ -567,3 +567,30 @@ def test_grid_on_small_scenes_vs_oracle(gpu, manifest, images, kflags):
             assert rays == fz["rays"], fz["name"]
     finally:
         gpu.set_scene(*gpu.default_scene())
+
+
+def test_pool_scratch_over_more_streams_than_slots(gpu):
+    """The pool kernel keeps per-stream scratch in 8 slots; rendering on 11 streams in rotation
+    (twice round) takes slots over from other streams -- in stream order, behind an event of the
+    previous owner's last launch, with no device-wide sync (advisor r5) -- and every render
+    still gives the one-stream bits."""
+    import torch
+
+    from learnraytracing_amd import _lib as L
+    w, h, frames, depth = 1280, 720, 4, 8
+    want = np.zeros((h, w, 4), np.float32)
+    want_rays = gpu.render_host(gpu.Job(width=w, height=h, frames=frames, max_depth=depth), want)
+    streams = [torch.cuda.Stream() for _ in range(11)]
+    bufs = [torch.zeros((h, w, 4), dtype=torch.float32, device="cuda") for _ in range(2 * len(streams))]
+    rays = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in bufs]
+    cur = torch.cuda.current_stream()
+    for s in streams:
+        s.wait_stream(cur)   # the zero fills come first
+    job = gpu.Job(width=w, height=h, frames=frames, max_depth=depth)
+    for i, b in enumerate(bufs):
+        gpu.render_tensor(job, b, rays[i], streams[i % len(streams)])
+        assert L.last_launch()["kernel"] == "pool_kernel"
+    torch.cuda.synchronize()
+    for i, b in enumerate(bufs):
+        _assert_bitwise(b.cpu().numpy(), want[..., :3], f"render {i} on stream {i % len(streams)}")
+        assert int(rays[i].item()) == want_rays
