@@ -22,14 +22,18 @@ Mray/s, the reference's own formula (src/cpu/main.cpp:188-189; rays counted as
 parallel.cpp:122,204). Inputs are resident in HBM (the scene is uploaded once); no
 host transfer is inside the timed region.
 
-Besides the timed region (unless --no-extra-legs):
+Besides the timed region (unless --no-extra-legs; the DrawTest legs first, then the W warmup
+steps, then the end-to-end and launch-alone legs, then the K timed steps -- the ~35 launches of
+those legs hold the render's load while the power controller raises the shader clock, which
+otherwise ramps through a short timed region, profiles/r6_g):
   * `ms_per_launch_alone`: the same launches one at a time on one stream, each kernel
     bracketed by HIP events the library records on that stream right around it
     (lrt_kernel_timing) -- the duration the roofline objects divide by; `ms_per_call_alone`:
     the same launches with the events around the whole render call (its other stream
     commands and dispatch included);
   * `end_to_end`: render (+ gather and assembly) + the D2H copy of the frame into pinned
-    host memory on rank 0, pipelined over two slots;
+    host memory on rank 0 (N = 1: packed to RGB, 12 B/pixel, 4 frames in flight), beside the
+    box's own pinned D2H bandwidth (`copy_ceiling_gbs`);
   * `cpu_baseline` (all host cores) and `cpu_baseline_1core`: the reference's own
     TraceRowJob body (oracle/_ref, rank 0 at N = 1 only, before the GPU is touched).
 
@@ -446,6 +450,22 @@ def main():
     from learnraytracing_amd.renderer import pack_rgb_tensor, render_tensor_to_frame, unshard_rgb_tensor
 
     lrt.InitializeTest()
+    # ---- the reference API as its own caller uses it (rank 0, N = 1): DrawTest per frame, on
+    # one device and split over two contexts of it (lrt_initialize_devices([0, 0]): the
+    # multi-device host path's own cost, rehearsed on the one GPU this process drives). Run
+    # first, on their own context: the config's render below starts from a fresh one.
+    drawtest = drawtest_multi = None
+    if extra and world == 1:
+        wd.enter("drawtest")
+        drawtest = drawtest_leg(lrt)
+        torch.cuda.synchronize()
+        lrt.ShutdownTest()
+        lrt.InitializeDevices([gpu, gpu])
+        drawtest_multi = drawtest_leg(lrt, frames=100)
+        drawtest_multi["devices"] = f"[{gpu}, {gpu}] (lrt_initialize_devices, direct exchange)"
+        lrt.ShutdownTest()
+        lrt.InitializeTest()
+        torch.cuda.synchronize()
     # --reserve-cus R: render on a CU-masked stream (lrt_stream_create) leaving R CUs to
     # other streams. Off by default: a kernel on another stream only starts beside the
     # persistent render once >= 8 CUs per XCD are free (64 CUs, -23 % render throughput;
@@ -469,7 +489,11 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
     nstreams = max(1, args.streams)
     nslots = max(2, nstreams)
-    bufs = [torch.zeros((max_rows, W, 4), dtype=torch.float32, device=dev) for _ in range(nslots)]
+    # the end-to-end leg's frames in flight: a render must not wait for the copy of the frame
+    # before it (2 slots serialised render and copy: 0.43 = 0.225 + 0.203 ms/step, profiles/r6_e);
+    # a multiple of the render streams, so that slot s is always rendered on stream s % nstreams
+    e2e_slots = 2 * nstreams if world == 1 else nslots
+    bufs = [torch.zeros((max_rows, W, 4), dtype=torch.float32, device=dev) for _ in range(max(nslots, e2e_slots))]
     rays = torch.zeros(1, dtype=torch.int64, device=dev)
     # remote exchange: rank 0's frames mapped into every rank; each render stores its finished
     # pixels there itself (no pack, gather or unshard launch per step)
@@ -505,7 +529,22 @@ def main():
     astream = torch.cuda.Stream(device=dev) if world > 1 else stream
     cstream = torch.cuda.Stream(device=dev)
     host = None   # pinned frame copies (end-to-end leg)
+    e2e_rgb = []  # N = 1: the packed RGB frames the end-to-end leg copies
+
+    def d2h_ceiling(src, dst, reps=10):
+        """Pinned D2H bandwidth of this box (GB/s): reps copies of src into the page-locked dst
+        on the copy stream, timed with events -- the end-to-end leg's own ceiling."""
+        with torch.cuda.stream(cstream):
+            dst.copy_(src, non_blocking=True)   # (first touch of the pinned pages, untimed)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(cstream)
+            for _ in range(reps):
+                dst.copy_(src, non_blocking=True)
+            e1.record(cstream)
+        e1.synchronize()
+        return src.numel() * 4 * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
     pending = []   # (mode, work, slot, d2h, rdone) of steps whose gather / D2H is not yet enqueued
+    slot_done = {}   # (slot, d2h) -> event: that slot's gather / assembly / copy has completed
 
     def finish(mode, work, slot, d2h, rdone):
         """Assemble slot's frame on rank 0 (after its gather), then optionally copy it to
@@ -523,23 +562,28 @@ def main():
         if d2h and rank == 0:
             cstream.wait_event(done if done is not None else rdone)
             with torch.cuda.stream(cstream):
-                host[slot].copy_(frames_out[slot] if gather_ex else bufs[slot], non_blocking=True)
+                host[slot].copy_(frames_out[slot] if gather_ex else e2e_rgb[slot] if world == 1 else bufs[slot],
+                                 non_blocking=True)
             done = torch.cuda.Event()
             done.record(cstream)
-        if done is not None:
-            rstreams[slot % nstreams].wait_event(done)
+        if done is not None:   # the slot's next render waits for its gather / copy (step())
+            slot_done[(slot, d2h)] = done
 
     def step(k, mode, d2h=False):
         """mode: "remote" (stores into rank 0's IPC frame), "rccl" (pack + gather + unshard), or
-        "local" (N = 1)."""
-        slot = k % nslots
+        "local" (N = 1). d2h: the end-to-end leg, which cycles over e2e_slots buffers."""
+        slot = k % (e2e_slots if d2h else nslots)
         rs = rstreams[k % nstreams]
+        prev = slot_done.pop((slot, d2h), None)
+        if prev is not None:   # (only this render waits: the stream's other renders run on)
+            rs.wait_event(prev)
         if mode == "remote":
             render_tensor_to_frame(job, bufs[slot], rays, shared.ptrs[slot], rs)
         else:
             lrt.render_tensor(job, bufs[slot], rays, rs)
         rdone = None
         if d2h and world == 1:
+            pack_rgb_tensor(bufs[slot], e2e_rgb[slot], rs)
             rdone = torch.cuda.Event()
             rdone.record(rs)
         work = None
@@ -566,13 +610,23 @@ def main():
     # stream-ordered pool for its per-launch buffers (overflow stack, sample planes)
     warmup = max(args.warmup, nstreams)
 
-    def timed(mode):
-        """warmup + K timed steps of `mode`: (seconds, counted rays of this rank)."""
+    warm = {}
+
+    def warmup_steps(mode):
+        """The W untimed warmup steps of `mode`; their own time is kept (warm[mode], ms per step)
+        as the record of a cold start (first launches record and sort the tile order)."""
         wd.enter(f"warmup_{mode}")
+        sync_all()
+        tw = time.perf_counter()
         for k in range(warmup):
             step(k, mode)
         drain()
+        torch.cuda.synchronize()
+        warm[mode] = (time.perf_counter() - tw) / warmup * 1e3
         sync_all()
+
+    def timed(mode):
+        """K timed steps of `mode`: (seconds, counted rays of this rank)."""
         rays.zero_()
         sync_all()
         wd.enter(f"timed_{mode}")
@@ -587,6 +641,82 @@ def main():
         return t1 - t0, float(rays.item())
 
     mode = ("remote" if remote else "rccl") if world > 1 else "local"
+    warmup_steps(mode)
+    remote = mode == "remote"
+    # ---- extra legs, BEFORE the timed region: end to end (D2H included), then each launch alone
+    # (the roofline's duration). Under a render's full load the shader clock starts near 2.18 GHz
+    # and the power controller raises it to ~2.39 GHz over ~50 launches (~13 ms); the cycles per
+    # wave stay the same (tools/clock_ramp.py, profiles/r6_g). Timed right after W warmup steps, a
+    # 20-step region measured that ramp (0.241 against 0.224 ms/step at the held clock). These
+    # legs are ~35 launches of the same render; the timed steps are unchanged.
+    alone_ms = e2e_s = call_ms = None
+    copy_ceiling = host_identical = None
+    e2e_steps = 0
+    if extra:
+        if rank == 0:
+            # N = 1: the frame leaves as packed RGB (12 of the 16 B per pixel: the render never
+            # writes alpha; lrt_pack_rgb on the render stream); N > 1: rank 0's assembled RGBA frame
+            shape = (H, W, 4) if world > 1 else tuple(bufs[0].shape[:2]) + (3,)   # --shard-of: the shard
+            host = [torch.empty(shape, dtype=torch.float32, pin_memory=True) for _ in range(e2e_slots)]
+            if world == 1:
+                e2e_rgb[:] = [torch.empty(shape, dtype=torch.float32, device=dev) for _ in range(e2e_slots)]
+                copy_ceiling = d2h_ceiling(e2e_rgb[0], host[0])
+        e2e_steps = max(1, min(args.steps, 20))
+        wd.enter("end_to_end")
+        if remote:   # a frame is complete once every rank's render of it is: barrier, then D2H
+            def e2e_step(k):
+                step(k, mode)
+                sync_all()
+                if rank == 0:
+                    host[k % nslots].copy_(shared.tensor(k % nslots))
+            for k in range(nslots):
+                e2e_step(k)
+            sync_all()
+            t2 = time.perf_counter()
+            for k in range(e2e_steps):
+                e2e_step(k)
+            e2e_s = time.perf_counter() - t2
+            dist.barrier()
+        else:
+            for k in range(e2e_slots):   # untimed: each pinned buffer's first copy maps its pages
+                step(k, mode, d2h=True)
+            drain()
+            sync_all()
+            t2 = time.perf_counter()
+            for k in range(e2e_steps):
+                step(k, mode, d2h=True)
+            drain()
+            torch.cuda.synchronize()
+            e2e_s = time.perf_counter() - t2
+            if world == 1:   # the last frame on the host, bit for bit the device's RGB
+                last = (e2e_steps - 1) % e2e_slots
+                host_identical = bool(torch.equal(host[last].view(torch.int32),
+                                                  bufs[last][..., :3].contiguous().cpu().view(torch.int32)))
+            if world > 1:
+                dist.barrier()
+        drain()
+        sync_all()
+        wd.enter("launch_alone")
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+        scratch = torch.zeros(1, dtype=torch.int64, device=dev)
+        L.check(L.lib().lrt_kernel_timing(1))
+        for k in range(args.steps):
+            ev[k][0].record(stream)
+            if remote:
+                render_tensor_to_frame(job, bufs[0], scratch, shared.ptrs[0], stream)
+            else:
+                lrt.render_tensor(job, bufs[0], scratch, stream)
+            ev[k][1].record(stream)
+        torch.cuda.synchronize()
+        call_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+        kt = (ctypes.c_float * args.steps)()
+        nk = ctypes.c_int(0)
+        L.check(L.lib().lrt_kernel_times(kt, args.steps, ctypes.byref(nk)))
+        L.check(L.lib().lrt_kernel_timing(0))
+        # one render kernel per launch: the kernel's own events; else the call's
+        alone_ms = sum(kt[:nk.value]) / nk.value if nk.value == args.steps else call_ms
+
     elapsed, timed_rays = timed(mode)
     launch_info = L.last_launch()
     exchange_legs = None
@@ -606,6 +736,7 @@ def main():
     if both and shared is not None:
         # the other exchange, same steps; then both legs' assembled frames, bit for bit, on rank 0
         other = "rccl" if mode == "remote" else "remote"
+        warmup_steps(other)
         e2, r2 = timed(other)
         wd.enter("exchange_legs")
         legs = {mode: (elapsed, timed_rays), other: (e2, r2)}
@@ -628,80 +759,6 @@ def main():
                                   "pack to RGB + RCCL gather (dist.gather over nccl = RCCL) to rank 0 + unshard")}
                      for i, m in enumerate(("remote", "rccl"))},
         }
-    remote = mode == "remote"
-
-    # ---- extra legs: each launch alone (roofline duration), end to end (D2H included)
-    alone_ms = e2e_s = call_ms = None
-    e2e_steps = 0
-    if extra:
-        wd.enter("launch_alone")
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps)]
-        scratch = torch.zeros(1, dtype=torch.int64, device=dev)
-        L.check(L.lib().lrt_kernel_timing(1))
-        for k in range(args.steps):
-            ev[k][0].record(stream)
-            if remote:
-                render_tensor_to_frame(job, bufs[0], scratch, shared.ptrs[0], stream)
-            else:
-                lrt.render_tensor(job, bufs[0], scratch, stream)
-            ev[k][1].record(stream)
-        torch.cuda.synchronize()
-        call_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
-        kt = (ctypes.c_float * args.steps)()
-        nk = ctypes.c_int(0)
-        L.check(L.lib().lrt_kernel_times(kt, args.steps, ctypes.byref(nk)))
-        L.check(L.lib().lrt_kernel_timing(0))
-        # one render kernel per launch: the kernel's own events; else the call's
-        alone_ms = sum(kt[:nk.value]) / nk.value if nk.value == args.steps else call_ms
-        if rank == 0:
-            shape = (H, W, 4) if world > 1 else tuple(bufs[0].shape)   # --shard-of: the shard itself
-            host = [torch.empty(shape, dtype=torch.float32, pin_memory=True) for _ in range(nslots)]
-        e2e_steps = max(1, min(args.steps, 10))
-        wd.enter("end_to_end")
-        if remote:   # a frame is complete once every rank's render of it is: barrier, then D2H
-            def e2e_step(k):
-                step(k, mode)
-                sync_all()
-                if rank == 0:
-                    host[k % nslots].copy_(shared.tensor(k % nslots))
-            for k in range(nslots):
-                e2e_step(k)
-            sync_all()
-            t2 = time.perf_counter()
-            for k in range(e2e_steps):
-                e2e_step(k)
-            e2e_s = time.perf_counter() - t2
-            dist.barrier()
-        else:
-            for k in range(nslots):   # untimed: each pinned buffer's first copy maps its pages
-                step(k, mode, d2h=True)
-            drain()
-            sync_all()
-            t2 = time.perf_counter()
-            for k in range(e2e_steps):
-                step(k, mode, d2h=True)
-            drain()
-            torch.cuda.synchronize()
-            e2e_s = time.perf_counter() - t2
-            if world > 1:
-                dist.barrier()
-
-    # ---- the reference API as its own caller uses it (rank 0, N = 1): DrawTest per frame, on
-    # one device and split over two contexts of it (lrt_initialize_devices([0, 0]): the
-    # multi-device host path's own cost, rehearsed on the one GPU this process drives)
-    if extra and world == 1:
-        wd.enter("drawtest")
-    drawtest = drawtest_leg(lrt) if extra and world == 1 else None
-    drawtest_multi = None
-    if extra and world == 1:
-        torch.cuda.synchronize()
-        lrt.ShutdownTest()
-        lrt.InitializeDevices([gpu, gpu])
-        drawtest_multi = drawtest_leg(lrt, frames=100)
-        drawtest_multi["devices"] = f"[{gpu}, {gpu}] (lrt_initialize_devices, direct exchange)"
-        lrt.ShutdownTest()
-        lrt.InitializeTest()
     torch.cuda.synchronize()
 
     wd.enter("stats")
@@ -783,6 +840,15 @@ def main():
             "ms_per_step": round(ms_step, 4),
             "ms_per_launch_alone": round(alone_ms, 4) if alone_ms else None,
             "ms_per_call_alone": round(call_ms, 4) if call_ms else None,
+            "ms_per_step_warmup": round(warm[mode], 4),
+            "timing_note": "ms_per_step: the K timed steps, pipelined over the render streams (a step's launch "
+                           "overlaps its neighbours' tails); ms_per_launch_alone: one launch with nothing beside "
+                           "it, the roofline's duration; ms_per_step_warmup: rank 0's W untimed warmup steps (first "
+                           "launches record the tile order). Order: W warmup steps, the end_to_end and launch-alone "
+                           "legs (~35 launches), then the K timed steps: under a render's load the shader clock "
+                           "rises from ~2.18 to ~2.39 GHz over ~50 launches at constant cycles per wave "
+                           "(profiles/r6_g), which a 20-step region right after the warmup measured (0.241 vs "
+                           "0.224 ms/step)",
             "higher_is_better": True,
             "scaling": args.scaling,
             "vs_baseline": None,
@@ -813,9 +879,14 @@ def main():
                 "value": round(total_rays / args.steps * e2e_steps / e2e_s / 1e6, 3), "unit": "Mray/s",
                 "ms_per_step": round(e2e_s / e2e_steps * 1e3, 4), "steps": e2e_steps,
                 "what": "render" + ((" + remote stores into rank 0's frame, barrier" if remote else
-                                     " + RCCL gather + assembly") if world > 1 else "")
-                        + " + D2H of the RGBA frame into pinned host memory on rank 0"
-                        + (", one step at a time" if remote else ", pipelined over 2 slots"),
+                                     " + RCCL gather + assembly") if world > 1 else " + pack to RGB")
+                        + (" + D2H of the RGBA frame" if world > 1 else " + D2H of the RGB frame (12 B/pixel)")
+                        + " into pinned host memory on rank 0"
+                        + (", one step at a time" if remote else f", pipelined over {e2e_slots} frames in flight"),
+                "copy_ceiling_gbs": round(copy_ceiling, 2) if copy_ceiling else None,
+                "copy_ms_at_ceiling": (round(H * W * 12 / (copy_ceiling * 1e9) * 1e3, 4)
+                                       if copy_ceiling and world == 1 else None),
+                "host_frame_identical": host_identical,
             } if e2e_s else None,
             "cpu_baseline": cpu,
             "cpu_baseline_1core": cpu1,

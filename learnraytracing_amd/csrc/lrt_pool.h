@@ -172,6 +172,7 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
 #endif
 #ifdef LRT_EXP_WAVETRACE
     const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long wc0 = __builtin_amdgcn_s_memtime();   // (LRT_EXP_WAVECLK: shader cycles)
     unsigned long long wlast = 0, wtiles = 0;   // the last task's start, the task count
 #endif
     float4* const lstk = smem + wave * kLv * 64 + lane;   // this lane's recursion stack (LDS)
@@ -513,7 +514,11 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
         a.wtrace[4 * wid + 2] = (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) |   // HW_ID
                                 ((unsigned long long)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32) |  // XCC_ID
                                 (wtiles << 40);
+#ifdef LRT_EXP_WAVECLK
+        a.wtrace[4 * wid + 3] = __builtin_amdgcn_s_memtime() - wc0;   // the wave's life in shader cycles
+#else
         a.wtrace[4 * wid + 3] = wlast;
+#endif
     }
 #endif
     const unsigned long long total = wave_sum((unsigned long long)rays);
