@@ -366,7 +366,16 @@ inline void kernel_timing(hipStream_t s, int which) {
 hipError_t occupancy(int* per_cu, const void* kern, int block, size_t lds);
 const char* acc_name(int acc);
 int pool_tiles(int pix, int xc, int rows);
-int pool_pixels(int frames, int xc, int rows);
+// Tile pixels of a pool launch: the largest power of two <= cap whose pool fits a round and,
+// above 64 px, still gives every resident wave a tile.
+int pool_pixels(int frames, int xc, int rows, int cap);
+// Largest pool tile for a launch that overlaps another stream's pool launch (lrt_render.hip).
+#ifndef LRT_POOL_PIX_OVERLAP
+#define LRT_POOL_PIX_OVERLAP 128
+#endif
+constexpr int kPoolPixOverlap = LRT_POOL_PIX_OVERLAP;
+// Is a pool launch of another stream than s still running (its scratch slot's last-use event)?
+hipError_t other_stream_busy(hipStream_t s, bool* busy);
 // sample mode's merge (merge_samples_kernel) on stream s
 hipError_t launch_merge_samples(const float4* samp, float4* out, const float* lerp, int npix, int frame0, int frames,
                                 size_t stride, const KernelArgs& a, int pix0, hipStream_t s);
@@ -374,7 +383,7 @@ int launch_wavefront(KernelArgs a, bool lds, hipStream_t s);
 // colours_out / frame: see the definition
 int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_rays, const lrt_features* feat,
                   hipStream_t s, float4* colours_out = nullptr, float* frame = nullptr);
-int auto_kernel(const KernelArgs& a, const lrt_render_desc* d, bool feat);
+int auto_kernel(const KernelArgs& a, const lrt_render_desc* d, bool feat, int pix_cap = 64);
 #ifdef LRT_EXP_WAVETRACE
 unsigned long long* wavetrace_buffer(size_t waves);
 void wavetrace_dump(unsigned long long* d, size_t waves, hipStream_t s);
@@ -389,8 +398,8 @@ void secstats_dump(const unsigned long long* d_sec, hipStream_t s);
 int launch_v0_d8(const KernelArgs& a, bool lds, int xc, int rows, int frames, bool feat, bool colours, hipStream_t s);
 int launch_v0_d64(const KernelArgs& a, bool lds, int xc, int rows, int frames, bool feat, bool colours, hipStream_t s);
 // ---- lrt_pool_d8.hip / lrt_pool_d64.hip
-int launch_pool_d8(const KernelArgs& a, bool lds, int xc, int rows, int frames, hipStream_t s);
-int launch_pool_d64(const KernelArgs& a, bool lds, int xc, int rows, int frames, hipStream_t s);
+int launch_pool_d8(const KernelArgs& a, bool lds, int xc, int rows, int frames, int pix_cap, hipStream_t s);
+int launch_pool_d64(const KernelArgs& a, bool lds, int xc, int rows, int frames, int pix_cap, hipStream_t s);
 
 // ---- lrt_order.hip
 bool pool_order_on();

@@ -24,12 +24,7 @@
 
 namespace lrt {
 
-enum : int { kPoolIdle = 0, kPoolTrace = 1, kPoolDone = 2, kPoolEnded = 3, kPoolRare = 4 };
-
-// Metal / Dielectric scatter deferral (A/B, LRT_POOL_DEFER=K lanes; 0 = off): see pool_kernel.
-#ifndef LRT_POOL_DEFER
-#define LRT_POOL_DEFER 0
-#endif
+enum : int { kPoolIdle = 0, kPoolTrace = 1, kPoolDone = 2, kPoolEnded = 3 };
 
 template <int kPix>
 struct PoolTile {   // tile shape: kPix pixels, as square as a power of two allows
@@ -238,7 +233,6 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
     unsigned long long* ctr = a.tiles + q * kCtrStride;
     // late tile reservation and issue priority by occupancy (below): the depth-8 one-wave instances
     constexpr bool kLate = kW == 1 && MAXD <= 8;
-    constexpr int kDefer = kLate ? LRT_POOL_DEFER : 0;
     for (int i = (int)(blockIdx.x / kV0Queues) * kW + wave; i < nq;) {
         const int task = q + kV0Queues * i;
         const int tile = a.perm ? a.perm[task] : task;   // heaviest-first order (tile_order)
@@ -334,7 +328,7 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
                     }
                 }
                 const unsigned long long traceM = __ballot(state == kPoolTrace);
-                if (traceM == 0 && (!kDefer || __ballot(state == kPoolRare) == 0)) {
+                if (traceM == 0) {
                     if (__ballot(state == kPoolIdle || state == kPoolEnded) == 0) break;   // the pool is dry
                     continue;
                 }
@@ -386,29 +380,8 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
                         const float t = 0.5f * (r.dir.y + 1.0f);
                         leaf = ((1.0f - t) * f3(1.0f, 1.0f, 1.0f) + t * f3(0.5f, 0.7f, 1.0f)) * 0.3f;
                         fin = true;
-                    } else if (kDefer && depth < a.maxDepth && __float_as_int(sc.mats[3 * nid].w) != 0) {
-                        // a Metal or Dielectric hit parks the path until enough lanes hold one (below):
-                        // its hit (nid, nt) waits in registers the path does not use until it scatters
-                        // (the pending light's, already consumed above)
-                        state = kPoolRare;
-                        dl.li = nid;
-                        carry.x = nt;
                     } else {
                         shade = true;
-                    }
-                }
-                if constexpr (kDefer) {
-                    // Parked paths scatter together once kDefer of them wait, or when no path is left
-                    // to trace: the Metal / Dielectric regions then run with more lanes (profiles/r6_*).
-                    // Each path's events keep their order and its RNG stream is its own: same bits.
-                    const unsigned long long rareM = __ballot(state == kPoolRare);
-                    if (rareM && (__popcll(rareM) >= kDefer || __ballot(shade) == 0)) {
-                        if (state == kPoolRare) {
-                            nid = dl.li;
-                            nt = carry.x;
-                            shade = true;
-                            state = kPoolTrace;
-                        }
                     }
                 }
                 if (shade) {   // HitWorld's winner (maths.cpp:74-76,86-88), then Scatter (:210-212)

@@ -3,8 +3,8 @@
 
 namespace lrt {
 
-int launch_pool_d8(const KernelArgs& a, bool lds, int xc, int rows, int frames, hipStream_t s) {
-    return launch_pool_split<8>(a, lds, xc, rows, frames, s);
+int launch_pool_d8(const KernelArgs& a, bool lds, int xc, int rows, int frames, int pix_cap, hipStream_t s) {
+    return launch_pool_split<8>(a, lds, xc, rows, frames, pix_cap, s);
 }
 
 }  // namespace lrt

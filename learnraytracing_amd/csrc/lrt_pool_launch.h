@@ -183,8 +183,8 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
 }
 
 template <int MAXD>
-int launch_pool_split(const KernelArgs& a, bool lds, int xc, int rows, int frames, hipStream_t s) {
-    switch (pool_pixels(frames, xc, rows)) {
+int launch_pool_split(const KernelArgs& a, bool lds, int xc, int rows, int frames, int pix_cap, hipStream_t s) {
+    switch (pool_pixels(frames, xc, rows, pix_cap)) {
         case 256: return launch_pool<MAXD, 256>(a, lds, xc, rows, s);
         case 128: return launch_pool<MAXD, 128>(a, lds, xc, rows, s);
         case 64: return launch_pool<MAXD, 64>(a, lds, xc, rows, s);

@@ -191,6 +191,17 @@ hipError_t stream_scratch(hipStream_t s, size_t bytes, void** out) {
     return hipSuccess;
 }
 
+hipError_t other_stream_busy(hipStream_t s, bool* busy) {
+    *busy = false;
+    for (auto& e : ctx().scratch)
+        if (e.p && e.s != s) {
+            bool done = false;
+            if (const hipError_t r = event_done(e.ev, &done)) return r;
+            if (!done) *busy = true;
+        }
+    return hipSuccess;
+}
+
 hipError_t stream_scratch_used(hipStream_t s) {
     for (auto& e : ctx().scratch)
         if (e.p && e.s == s) return hipEventRecord(e.ev, s);
@@ -227,8 +238,7 @@ int pool_tiles(int pix, int xc, int rows) {
     const int tx = pix >= 128 ? 16 : pix >= 32 ? 8 : pix >= 8 ? 4 : pix >= 2 ? 2 : 1, ty = pix / tx;
     return ((xc + tx - 1) / tx) * ((rows + ty - 1) / ty);
 }
-int pool_pixels(int frames, int xc, int rows) {
-    constexpr int cap = 64;   // largest tile (128 px: +4 % pipelined, +25-35 % alone, profiles/r3_ag)
+int pool_pixels(int frames, int xc, int rows, int cap) {
     const long long slots = 16LL * ctx().num_cus;   // resident waves (4 per SIMD)
     for (int pix : {256, 128, 64, 32, 16})
         if (cap >= pix && pix * frames <= kPoolSamples && (pix <= 64 || pool_tiles(pix, xc, rows) >= slots))
@@ -433,14 +443,25 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
         return launch_v0_d64(a, lds, d->x_count, d->row_count, d->frames, false, true, s);
     }
     int kflags = d->flags & (LRT_F_SIMPLE | LRT_F_WAVEFRONT | LRT_F_POOL);
-    if (kflags == 0) kflags = auto_kernel(a, d, want_feat);
+    // Pool tiles: 64 px, or 128 px when another stream's pool launch is still running, i.e. this
+    // launch will overlap it. A 128-px tile is a pool of twice the samples, so a pool's drain (its
+    // last paths finishing with most lanes idle) is paid half as often, but with ~1.8 tiles per
+    // wave the launch's own tail grows; beside another launch that tail is filled (config 2 two
+    // streams 0.2237 -> 0.2104 ms/step, one stream 0.2564 -> 0.2717 with 128 px, profiles/r6_k).
+    int pix_cap = 64;
+    if (!(kflags & (LRT_F_SIMPLE | LRT_F_WAVEFRONT)) && d->frames >= 4) {
+        bool busy = false;
+        if (const hipError_t e = other_stream_busy(s, &busy)) return hip_fail(e, "pool launch events");
+        if (busy) pix_cap = kPoolPixOverlap;
+    }
+    if (kflags == 0) kflags = auto_kernel(a, d, want_feat, pix_cap);
     if (want_feat && !(kflags & LRT_F_SIMPLE))
         return fail(LRT_E_INVALID, "features are implemented by the v0 kernel only");
     if (kflags & LRT_F_WAVEFRONT) return launch_wavefront(a, lds, s);
     if (kflags & LRT_F_POOL) {
         a.colbuf = nullptr;
-        if (d->max_depth <= 8) return launch_pool_d8(a, lds, d->x_count, d->row_count, d->frames, s);
-        return launch_pool_d64(a, lds, d->x_count, d->row_count, d->frames, s);
+        if (d->max_depth <= 8) return launch_pool_d8(a, lds, d->x_count, d->row_count, d->frames, pix_cap, s);
+        return launch_pool_d64(a, lds, d->x_count, d->row_count, d->frames, pix_cap, s);
     }
     if (d->max_depth <= 8) return launch_v0_d8(a, lds, d->x_count, d->row_count, d->frames, want_feat, false, s);
     // depth 9..64: one instance (MAXD only decides whether stack levels beyond the 8 in LDS
@@ -454,10 +475,10 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
 // heaviest-first tile order (tile_order), the 8-bounce default scene too (config 2: 0.254 vs
 // 0.289 ms/step, 0.297 vs 0.329 ms for a launch alone); v0 otherwise (few pixels with many
 // frames, a GPU's row shard, take v0's frame lanes and sample mode; features are v0's).
-int auto_kernel(const KernelArgs& a, const lrt_render_desc* d, bool feat) {
+int auto_kernel(const KernelArgs& a, const lrt_render_desc* d, bool feat, int pix_cap) {
     if (feat || d->frames < 4) return LRT_F_SIMPLE;
     if (!(a.bv.on || a.gv.on || d->max_depth > 8) && !pool_order_on()) return LRT_F_SIMPLE;
-    const int pix = pool_pixels(d->frames, d->x_count, d->row_count);
+    const int pix = pool_pixels(d->frames, d->x_count, d->row_count, pix_cap);
     const long long tiles = pool_tiles(pix, d->x_count, d->row_count);
     const long long slots = 16LL * ctx().num_cus;   // resident waves (4 per SIMD)
     // at least a tile per resident wave: config 2's row shard of 2 (7,200 tiles) runs 0.1316 ms

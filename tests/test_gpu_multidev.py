@@ -221,23 +221,31 @@ def test_pool_order_two_streams_bitwise(gpu):
     host synchronisation in between: the order is sorted on the device behind the recording
     launch, the second launch (the other stream) records again in that order and sorts into the
     other permutation buffer (order=5), and every later launch, on either stream, waits for the
-    latest sort's event. Every frame equals the single-stream render."""
+    latest sort's event. Every frame equals the single-stream render. A launch made while the
+    other stream's is still running takes 128-px tiles (a signature, and an order, of its own):
+    per tile size, the orders run recording -> refining (5) -> sorted (2)."""
     import torch
     from learnraytracing_amd import _lib as L
     w, h = 1280, 720
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
     outs = [torch.zeros((h, w, 4), dtype=torch.float32, device="cuda") for _ in range(8)]
-    orders = []
+    orders, pix = [], []
     cam = gpu.make_camera((0.1, 2, 3), (0, 0, 0), (0, 1, 0), 60, w / h, 0.1, 3)   # a signature of its own
     job2 = gpu.Job(width=w, height=h, frames=4, max_depth=8, camera=cam)
     for k, o in enumerate(outs):
         _torch_render(gpu, job2, streams[k % 2], o)
-        orders.append(L.last_launch()["order"])
+        info = L.last_launch()
+        orders.append(info["order"])
+        pix.append(info["pix"])
     torch.cuda.synchronize()
     want, _ = oracle.orc_render(w, h, 4, 8, cam22=cam.to22())
     for k, o in enumerate(outs):
         _bitwise(o.cpu().numpy(), want, f"launch {k} (order {orders[k]})")
-    assert orders[0] in ("1", "3", "4") and orders[1] == "5" and orders[2:] == ["2"] * 6, orders
+    for p in set(pix):
+        seq = [o for o, q in zip(orders, pix) if q == p]
+        assert seq[0] in ("1", "3", "4") and seq[1:2] in (["5"], []) and seq[2:] == ["2"] * (len(seq) - 2), \
+            (orders, pix)
+    assert set(pix) <= {"64", "128"} and "128" in pix, (orders, pix)   # the overlapping launches' tiles
 
 
 def test_config2_benchmarked_state_vs_oracle(gpu):
