@@ -57,9 +57,9 @@ int lrt_scatter_eval(const lrt_sphere* spheres, const lrt_material* materials, i
                      int n, float* out, int* ret, int* counted, uint32_t* state, int on_device);
 
 /* ---- kernel timing (bench.py's launch-alone leg) ------------------------------- */
-/* on != 0: every later render kernel launch (the pool kernel and v0) on the current device is
- * bracketed by two HIP events recorded on its own stream, right before and after the kernel --
- * no other stream command in between; on = 0 stops and discards them. lrt_kernel_times waits
+/* on != 0: every later render kernel launch (the pool kernel and v0), on whichever device it
+ * runs, is bracketed by two HIP events of that device recorded on its own stream, right before
+ * and after the kernel -- no other stream command in between; on = 0 stops and discards them. lrt_kernel_times waits
  * for the recorded launches and writes up to max_n durations (ms) in launch order to ms, their
  * number to *n, then forgets them. */
 int lrt_kernel_timing(int on);

@@ -91,21 +91,43 @@ using namespace lrt;
 
 namespace lrt {
 bool g_ktiming_on = false;
-std::vector<std::pair<hipEvent_t, hipEvent_t>> g_ktiming_ev;   // (start, stop) per recorded launch
+// (start, stop, device) per recorded launch: events belong to the device current at their
+// creation, and a launch on another device (render_host_multi, a second context) gets a pair of
+// its own device's (advisor r5: a process-global pool recorded foreign-device events)
+struct KTiming {
+    hipEvent_t a, b;
+    int dev;
+};
+std::vector<KTiming> g_ktiming_ev;
 size_t g_ktiming_used = 0;
 void kernel_timing_mark(hipStream_t s, int which) {
     if (which == 0) {
-        if (g_ktiming_used == g_ktiming_ev.size()) {
+        int dev = -1;
+        if (hipGetDevice(&dev) != hipSuccess) {
+            g_ktiming_on = false;   // (diagnostic only: stop rather than fail the render)
+            return;
+        }
+        if (g_ktiming_used < g_ktiming_ev.size() && g_ktiming_ev[g_ktiming_used].dev != dev) {
+            int cur = -1;   // this slot's events are another device's: replace them
+            KTiming& k = g_ktiming_ev[g_ktiming_used];
+            (void)hipGetDevice(&cur);
+            (void)hipSetDevice(k.dev);
+            (void)hipEventDestroy(k.a);
+            (void)hipEventDestroy(k.b);
+            (void)hipSetDevice(cur);
+            g_ktiming_ev.erase(g_ktiming_ev.begin() + (long)g_ktiming_used);
+        }
+        if (g_ktiming_used >= g_ktiming_ev.size()) {
             hipEvent_t a = nullptr, b = nullptr;
             if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
-                g_ktiming_on = false;   // (diagnostic only: stop rather than fail the render)
+                g_ktiming_on = false;
                 return;
             }
-            g_ktiming_ev.emplace_back(a, b);
+            g_ktiming_ev.insert(g_ktiming_ev.begin() + (long)g_ktiming_used, KTiming{a, b, dev});
         }
-        (void)hipEventRecord(g_ktiming_ev[g_ktiming_used].first, s);
+        if (hipEventRecord(g_ktiming_ev[g_ktiming_used].a, s) != hipSuccess) g_ktiming_on = false;
     } else {
-        (void)hipEventRecord(g_ktiming_ev[g_ktiming_used].second, s);
+        if (hipEventRecord(g_ktiming_ev[g_ktiming_used].b, s) != hipSuccess) g_ktiming_on = false;
         ++g_ktiming_used;
     }
 }
@@ -435,9 +457,9 @@ int lrt_kernel_times(float* ms, int max_n, int* n) {
     int k = 0;
     for (size_t i = 0; i < lrt::g_ktiming_used && k < max_n; ++i) {
         auto& p = lrt::g_ktiming_ev[i];
-        LRT_HIP(hipEventSynchronize(p.second));
+        LRT_HIP(hipEventSynchronize(p.b));
         float t = 0.0f;
-        LRT_HIP(hipEventElapsedTime(&t, p.first, p.second));
+        LRT_HIP(hipEventElapsedTime(&t, p.a, p.b));
         ms[k++] = t;
     }
     *n = k;

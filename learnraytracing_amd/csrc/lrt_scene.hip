@@ -358,12 +358,26 @@ hipError_t upload(T*& d, const std::vector<T>& h) {   // a device copy (at least
     return e;
 }
 
-// The BVH's and the grid's device copies (upload_scene, or later on first use: ensure_*).
+template <class T>
+static void free_dev(T*& d) {
+    if (d) (void)hipFree(d);
+    d = nullptr;
+}
+// The BVH's and the grid's device copies (upload_scene, or later on first use: ensure_*). A failed
+// upload frees what it had allocated and leaves the structure unbuilt (the next ensure_* starts
+// from nothing instead of allocating over the earlier buffers: advisor r5).
 static int upload_bvh(Context& c, BvhHost& B) {
     if (B.nodes.empty()) B.nodes.assign(4, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-    LRT_HIP(upload(c.d_bvh_nodes, B.nodes));
-    LRT_HIP(upload(c.d_bvh_lsph, B.lsph));
-    LRT_HIP(upload(c.d_bvh_lid, B.lid));
+    hipError_t e = upload(c.d_bvh_nodes, B.nodes);
+    if (e == hipSuccess) e = upload(c.d_bvh_lsph, B.lsph);
+    if (e == hipSuccess) e = upload(c.d_bvh_lid, B.lid);
+    if (e != hipSuccess) {
+        free_dev(c.d_bvh_nodes);
+        free_dev(c.d_bvh_lsph);
+        free_dev(c.d_bvh_lid);
+        c.bvh_built = false;
+        return hip_fail(e, "BVH upload");
+    }
     bvh_view_host(B, c.bvh);
     c.bvh.nodes = c.d_bvh_nodes;
     c.bvh.lsph = c.d_bvh_lsph;
@@ -373,11 +387,20 @@ static int upload_bvh(Context& c, BvhHost& B) {
     return LRT_OK;
 }
 static int upload_grid(Context& c, const GridHost& G) {
-    LRT_HIP(upload(c.d_grid_cells, G.ranges));
-    LRT_HIP(upload(c.d_grid_rsph, G.rsph));
-    LRT_HIP(upload(c.d_grid_rid, G.rid));
-    LRT_HIP(upload(c.d_grid_bsph, G.bsph));
-    LRT_HIP(upload(c.d_grid_bid, G.bid));
+    hipError_t e = upload(c.d_grid_cells, G.ranges);
+    if (e == hipSuccess) e = upload(c.d_grid_rsph, G.rsph);
+    if (e == hipSuccess) e = upload(c.d_grid_rid, G.rid);
+    if (e == hipSuccess) e = upload(c.d_grid_bsph, G.bsph);
+    if (e == hipSuccess) e = upload(c.d_grid_bid, G.bid);
+    if (e != hipSuccess) {
+        free_dev(c.d_grid_cells);
+        free_dev(c.d_grid_rsph);
+        free_dev(c.d_grid_rid);
+        free_dev(c.d_grid_bsph);
+        free_dev(c.d_grid_bid);
+        c.grid_built = false;
+        return hip_fail(e, "grid upload");
+    }
     GridView& g = c.gv;
     g = grid_view_host(G, c.d_sph);
     g.cells = c.d_grid_cells;
@@ -396,7 +419,9 @@ static void pack_spheres(const std::vector<lrt_sphere>& s, std::vector<float4>& 
 // The BVH is built when the policy picks it at lrt_set_scene, else on the first render that
 // asks for it (LRT_F_BVH, a feature launch, the wavefront kernels); the grid when the policy
 // needs it (scenes above kBvhMinSpheres, unless LRT_ACCEL=bvh), else on the first LRT_F_GRID
-// render. (advisor r4: every scene used to pay for both builds and both uploads.)
+// render. (advisor r4: every scene used to pay for both builds and both uploads.) A structure
+// built lazily can therefore fail at that render (LRT_E_HIP / LRT_E_INVALID from
+// lrt_render_*), not at lrt_set_scene; the scene itself stays in place.
 int ensure_bvh(Context& c) {
     if (c.bvh_built || !c.bvh_on) return LRT_OK;
     std::vector<float4> sph;
