@@ -883,6 +883,8 @@ def main():
                         + (" + D2H of the RGBA frame" if world > 1 else " + D2H of the RGB frame (12 B/pixel)")
                         + " into pinned host memory on rank 0"
                         + (", one step at a time" if remote else f", pipelined over {e2e_slots} frames in flight"),
+                "frames_in_flight": e2e_slots if not remote else 1,
+                "untimed_steps": e2e_slots if not remote else nslots,
                 "copy_ceiling_gbs": round(copy_ceiling, 2) if copy_ceiling else None,
                 "copy_ms_at_ceiling": (round(H * W * 12 / (copy_ceiling * 1e9) * 1e3, 4)
                                        if copy_ceiling and world == 1 else None),

@@ -74,8 +74,9 @@ def main():
                 summary["kernel_trace"] = {"name": r["Name"], "calls": int(r["Calls"]),
                                            "avg_ns": float(r["AverageNs"]), "min_ns": float(r["MinNs"]),
                                            "max_ns": float(r["MaxNs"]), "percent": float(r["Percentage"])}
-    # the launch-alone leg of the traced bench run: launches [warmup + steps, warmup + 2 steps)
-    # in dispatch order (bench.py), the leg whose HIP-event average the bench line divides by
+    # the launch-alone leg of the traced bench run, in dispatch order (bench.py, round 6): the W
+    # warmup launches, the end-to-end leg's untimed frames in flight and its timed steps, then the
+    # alone leg's `steps` launches -- the leg whose HIP-event average the bench line divides by
     bench_line = None
     for f in glob.glob(os.path.join(prof, f"trace_c{c}_*.log")):
         for line in open(f, errors="replace"):
@@ -85,7 +86,8 @@ def main():
         rows = sorted((r for r in csv.DictReader(open(f)) if is_render(r["Kernel_Name"])),
                       key=lambda r: int(r["Start_Timestamp"]))
         if bench_line and bench_line.get("ms_per_launch_alone"):
-            a = bench_line["warmup"] + bench_line["steps"]
+            e2e = bench_line.get("end_to_end") or {}
+            a = bench_line["warmup"] + e2e.get("untimed_steps", 0) + e2e.get("steps", 0)
             d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) for r in rows[a:a + bench_line["steps"]]]
             if d:
                 summary["alone_leg"] = {"launches": len(d), "avg_ns": sum(d) / len(d), "min_ns": min(d),
