@@ -416,15 +416,17 @@ def main():
 
     backend = os.environ.get("LRT_DIST_BACKEND", "nccl")   # nccl = RCCL; gloo only to rehearse on 1 GPU
     # LRT_BENCH_SAME_GPU=1 puts every rank on GPU 0 (rehearsing the RCCL path on a 1-GPU box)
-    gpu = 0 if (backend != "nccl" or os.environ.get("LRT_BENCH_SAME_GPU") == "1") else local_rank
+    one_gpu = backend != "nccl" or os.environ.get("LRT_BENCH_SAME_GPU") == "1"
+    gpu = 0 if one_gpu else local_rank
     def check_devices():
         """Refuse a world the visible GPUs cannot hold (one rank per GPU over RCCL), rank 0
         printing the line -- never fewer GPUs than the line's n_gpus. (Counting devices does
         not initialise the GPU.)"""
         ndev = torch.cuda.device_count()
-        if gpu < ndev and not (backend == "nccl" and gpu == local_rank and world > ndev):
+        need = 1 if one_gpu else world
+        if ndev >= need:
             return
-        msg = f"--gpus {world} needs {world if gpu == local_rank else 1} visible GPU(s), {ndev} visible"
+        msg = f"--gpus {world} needs {need} visible GPU(s), {ndev} visible"
         if rank == 0:
             line = dict(wd.base)
             line.update({"error": msg, "failed_phase": "device_count"})
