@@ -257,3 +257,21 @@ def test_bench_gpus_2_self_launches(gpu):
     d = lines[0]
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["rays_per_step"] == 11669343, d
     assert d["exchange"]["frames_identical"] is True, d["exchange"]
+
+
+def test_bench_gpus_4_self_launches_remote_and_rccl(gpu):
+    """Four ranks on GPU 0 (more than the two the other tests use): `bench.py --gpus 4`, no
+    launcher, config 2 -- the row-block-cyclic shards of 4, both exchanges timed, rank 0's two
+    assembled frames identical, and config 2's own ray count across the four shards."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["LRT_DIST_BACKEND"] = "gloo"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "3", "--warmup", "1",
+           "--no-cpu-baseline"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=170)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = lines[0]
+    assert d["n_gpus"] == 4 and d["config"]["rays_per_step"] == 11669343, d
+    ex = d["exchange"]
+    assert ex["frames_identical"] is True and set(ex["legs"]) == {"remote", "rccl"}, ex
