@@ -97,6 +97,8 @@ struct KernelArgs {
     float4* samp;                 // sample mode: frames planes of xc * rows colours
     float* colbuf;                // v5 (pool): poolSlots colour slots (RGB) per block
     int poolSlots;
+    int splitFrom;                // v5: queue items from here on are half tiles (lrt_pool.h)
+    int split16;                  // v5 (host): sixteenths of the tiles served as halves (launch_pool)
     const int* perm;              // v5: queue position -> tile, heaviest measured tiles first (null: identity)
     unsigned* tcost;              // v5: per-tile cost recording (100 MHz ticks of the tile's wave), or null
     int sampOnly;                 // colours only (the pipelined host path): samp is the caller's
@@ -374,6 +376,16 @@ int pool_pixels(int frames, int xc, int rows, int cap);
 #define LRT_POOL_PIX_OVERLAP 128
 #endif
 constexpr int kPoolPixOverlap = LRT_POOL_PIX_OVERLAP;
+// Sixteenths of a launch's (lightest) tiles served as halves, alone and overlapped (launch_pool;
+// config 2 alone 0.2580-0.2586 -> 0.2538-0.2558 ms at 5/16, 3/16 and 8/16 less, profiles/r6_v)
+#ifndef LRT_POOL_SPLIT16_ALONE
+#define LRT_POOL_SPLIT16_ALONE 5
+#endif
+#ifndef LRT_POOL_SPLIT16_OVERLAP
+#define LRT_POOL_SPLIT16_OVERLAP 0
+#endif
+constexpr int kPoolSplit16Alone = LRT_POOL_SPLIT16_ALONE;
+constexpr int kPoolSplit16Overlap = LRT_POOL_SPLIT16_OVERLAP;
 // Is a pool launch of another stream than s still running (its scratch slot's last-use event)?
 hipError_t other_stream_busy(hipStream_t s, bool* busy);
 // sample mode's merge (merge_samples_kernel) on stream s

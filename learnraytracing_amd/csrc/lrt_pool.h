@@ -217,9 +217,19 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
     float* const slots = a.colbuf + (size_t)wid * a.poolSlots * 3;
 
     constexpr int TX = PoolTile<kPix>::X, TY = PoolTile<kPix>::Y;
-    constexpr int kRoundFrames = kPoolSamples / kPix;
+    constexpr int kLgPix = kPix >= 256 ? 8 : kPix >= 128 ? 7 : kPix >= 64 ? 6 : kPix >= 32 ? 5 : kPix >= 16 ? 4
+                         : kPix >= 8 ? 3 : kPix >= 4 ? 2 : kPix >= 2 ? 1 : 0;
+    constexpr int kLgTX = TX >= 16 ? 4 : TX >= 8 ? 3 : TX >= 4 ? 2 : TX >= 2 ? 1 : 0;
+    static_assert((1 << kLgPix) == kPix && (1 << kLgTX) == TX, "tiles: powers of two");
     const int tilesX = (a.xc + TX - 1) / TX;
     const int ntiles = tilesX * ((a.rows + TY - 1) / TY);
+    // Split tail (a.splitFrom; the depth-8 one-wave linear-scan instances, whose launches have
+    // few tiles per wave): the queue's items from splitFrom on are the last -- lightest, in
+    // heaviest-first order -- tiles' left and right halves, so that a launch alone ends at
+    // half-tile granularity while its other pools keep the full tile's size (launch_pool).
+    constexpr bool kSplit = kW == 1 && TX >= 2 && MAXD <= 8 && kAcc == kAccScan;
+    const int splitFrom = kSplit ? (a.splitFrom < ntiles ? a.splitFrom : ntiles) : ntiles;
+    const int nitems = ntiles + (ntiles - splitFrom);
     const float invWidth = 1.0f / (float)a.width;     // parallel.cpp:260
     const float invHeight = 1.0f / (float)a.height;   // parallel.cpp:261
     const int fend = a.frame0 + a.frames;
@@ -229,19 +239,27 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
     // (kW > 1: the block's waves share its queue, so that a queue's counters stay in one XCD)
     const int q = blockIdx.x % kV0Queues;
     const int bq = (((int)gridDim.x - q + kV0Queues - 1) / kV0Queues) * kW;   // waves serving queue q
-    const int nq = (ntiles - q + kV0Queues - 1) / kV0Queues;
+    const int nq = (nitems - q + kV0Queues - 1) / kV0Queues;
     unsigned long long* ctr = a.tiles + q * kCtrStride;
     // late tile reservation and issue priority by occupancy (below): the depth-8 one-wave instances
     constexpr bool kLate = kW == 1 && MAXD <= 8;
     for (int i = (int)(blockIdx.x / kV0Queues) * kW + wave; i < nq;) {
         const int task = q + kV0Queues * i;
-        const int tile = a.perm ? a.perm[task] : task;   // heaviest-first order (tile_order)
+        // a whole tile, or (task >= splitFrom) one half of a tail tile
+        const int h = task - splitFrom;
+        const bool half = kSplit && h >= 0;
+        const int ord = half ? splitFrom + (h >> 1) : task;
+        const int tile = a.perm ? a.perm[ord] : ord;   // heaviest-first order (tile_order)
         const unsigned long long tt0 = a.tcost ? __builtin_amdgcn_s_memrealtime() : 0ull;
 #ifdef LRT_EXP_WAVETRACE
         wlast = __builtin_amdgcn_s_memrealtime();
         ++wtiles;
 #endif
-        const int tx0 = (tile % tilesX) * TX, ty0 = (tile / tilesX) * TY;
+        // the pool: 2^lgP pixels in rows of 2^lgW from (tx0, ty0)
+        const int lgW = half ? kLgTX - 1 : kLgTX;
+        const int lgP = half ? kLgPix - 1 : kLgPix;
+        const int tx0 = (tile % tilesX) * TX + (half ? (h & 1) << lgW : 0), ty0 = (tile / tilesX) * TY;
+        const int roundFrames = kPoolSamples >> lgP;
         // The next tile is reserved (queue atomic) at this tile's start, which hides the atomic's
         // latency behind the whole tile -- or, in launches of few tiles per wave (a.lateFetch:
         // config 2 has 3.5), once this tile's last samples are handed out: a tile reserved at the
@@ -254,9 +272,9 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
         unsigned long long fetched = 0;
         bool asked = !(kLate && a.lateFetch);
         if (asked && lane == 0) fetched = atomicAdd(ctr, 1ull);   // consumed after the tile
-        for (int fr0 = a.frame0; fr0 < fend; fr0 += kRoundFrames) {
-            const int nfr = fend - fr0 < kRoundFrames ? fend - fr0 : kRoundFrames;
-            const int N = nfr * kPix;   // this round's pool
+        for (int fr0 = a.frame0; fr0 < fend; fr0 += roundFrames) {
+            const int nfr = fend - fr0 < roundFrames ? fend - fr0 : roundFrames;
+            const int N = nfr << lgP;   // this round's pool
             int next = 0, state = kPoolIdle, k = 0, depth = 0;
             bool prevLambert = false;
             uint32_t rng = 1;
@@ -297,8 +315,8 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
                         k = next + __popcll(needM & below);
                         state = kPoolDone;
                         if (k < N) {
-                            const int j = k % kPix, f = fr0 + k / kPix;
-                            const int lx = tx0 + j % TX, ly = ty0 + j / TX;
+                            const int j = k & ((1 << lgP) - 1), f = fr0 + (k >> lgP);
+                            const int lx = tx0 + (j & ((1 << lgW) - 1)), ly = ty0 + (j >> lgW);
                             const KArgPtr pa = opaque_args();   // window and camera, read here
                             if (lx < pa->xc && ly < pa->rows) {   // TraceRowJob's per-pixel body (:270-279)
                                 sec_count(sc, kSecCamera);
@@ -321,7 +339,7 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
                     }
                     next += __popcll(needM);
                     if constexpr (kLate) {
-                        if (!asked && next >= N && fr0 + kRoundFrames >= fend) {   // the tile's last samples
+                        if (!asked && next >= N && fr0 + roundFrames >= fend) {   // the tile's last samples
                             if (lane == 0) fetched = atomicAdd(ctr, 1ull);
                             asked = true;
                         }
@@ -432,16 +450,15 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
             float4* const out = pa->out;
             const float* const lerp = pa->lerp;
             float4* const frame = pa->frame;
-#pragma unroll
-            for (int j0 = 0; j0 < kPix; j0 += 64) {   // tiles above 64 pixels: several per lane
+            for (int j0 = 0; j0 < (1 << lgP); j0 += 64) {   // pools above 64 pixels: several per lane
                 const int j = j0 + lane;
-                const int mx = tx0 + j % TX, my = ty0 + (j / TX) % TY;
-                if (j < kPix && mx < xc && my < rows) {
+                const int mx = tx0 + (j & ((1 << lgW) - 1)), my = ty0 + (j >> lgW);
+                if (j < (1 << lgP) && mx < xc && my < rows) {
                     float4* const mpx = out + (size_t)my * xc + mx;
                     float4 acc = *mpx;
                     F3 c3 = f3(acc.x, acc.y, acc.z);
                     for (int t = 0; t < nfr; ++t) {
-                        const float* const cp = slots + 3 * (t * kPix + j);
+                        const float* const cp = slots + 3 * ((t << lgP) + j);
                         const F3 c = f3(cp[0], cp[1], cp[2]);
                         const int f = fr0 + t;
                         const float lerpFac = f < kLerpTable ? lerp[f] : (float)f / (float)(f + 1);

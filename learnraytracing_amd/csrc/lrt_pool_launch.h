@@ -116,6 +116,12 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     int record = 0;
     Context::TileOrder* users[2];
     if (int rc = tile_order(a, kPix, ntiles, record, users, s)) return rc;
+    // the split tail: the last split16/16 of the (heaviest-first) tiles served as halves, in
+    // launches of few tiles per wave (a.lateFetch) that give every queue a block (the halves are
+    // extra queue items: a queue without a block would leave them undone); a recording launch
+    // times whole tiles
+    const bool split = !a.tcost && wpb == 1 && a.lateFetch && blocks >= kV0Queues;
+    a.splitFrom = split ? (int)(ntiles - ntiles * a.split16 / 16) : (int)ntiles;
     bool probed = false;
     if (record == 1 && pool_probe_mode() > 0 && (pool_probe_mode() == 2 || !users[1])) {
         // no measured order to go by: probe the tiles' costs, sort them, and let this
@@ -170,9 +176,10 @@ int launch_pool(KernelArgs a, bool lds, int xc, int rows, hipStream_t s) {
     // sorted order, 3 recording with the order borrowed from the same geometry, 4 recording in
     // the probe's order, 5 the refining pass (recording in the first pass's sorted order)
     snprintf(g_last_launch, sizeof(g_last_launch),
-             "kernel=pool_kernel maxd=%d lds=%d bvh=%d acc=%s pix=%d ns=%d grid=%u tasks=%lld order=%d per_cu=%d wpb=%d",
+             "kernel=pool_kernel maxd=%d lds=%d bvh=%d acc=%s pix=%d ns=%d grid=%u tasks=%lld order=%d per_cu=%d wpb=%d "
+             "split_from=%d",
              MAXD, lds ? 1 : 0, acc == kAccBvh ? 1 : 0, acc_name(acc), kPix, fixed ? kFixedSpheres : 0, grid.x, ntiles,
-             !users[0] ? 0 : !record ? 2 : record == 2 ? 5 : probed ? 4 : users[1] ? 3 : 1, per_cu, wpb);
+             !users[0] ? 0 : !record ? 2 : record == 2 ? 5 : probed ? 4 : users[1] ? 3 : 1, per_cu, wpb, a.splitFrom);
 #ifdef LRT_EXP_SECSTATS
     secstats_dump(d_sec, s);
 #endif

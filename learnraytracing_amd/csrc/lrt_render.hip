@@ -448,11 +448,18 @@ int render_device(const lrt_render_desc* d, float* d_buf, unsigned long long* d_
     // last paths finishing with most lanes idle) is paid half as often, but with ~1.8 tiles per
     // wave the launch's own tail grows; beside another launch that tail is filled (config 2 two
     // streams 0.2237 -> 0.2104 ms/step, one stream 0.2564 -> 0.2717 with 128 px, profiles/r6_k).
-    int pix_cap = 64;
+#ifndef LRT_POOL_PIX_ALONE
+#define LRT_POOL_PIX_ALONE 64   // (A/B builds: the tile cap of a launch alone)
+#endif
+    int pix_cap = LRT_POOL_PIX_ALONE;
+    a.split16 = kPoolSplit16Alone;
     if (!(kflags & (LRT_F_SIMPLE | LRT_F_WAVEFRONT)) && d->frames >= 4) {
         bool busy = false;
         if (const hipError_t e = other_stream_busy(s, &busy)) return hip_fail(e, "pool launch events");
-        if (busy) pix_cap = kPoolPixOverlap;
+        if (busy) {
+            pix_cap = kPoolPixOverlap;
+            a.split16 = kPoolSplit16Overlap;
+        }
     }
     if (kflags == 0) kflags = auto_kernel(a, d, want_feat, pix_cap);
     if (want_feat && !(kflags & LRT_F_SIMPLE))
