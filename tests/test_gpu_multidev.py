@@ -264,6 +264,8 @@ def test_config2_benchmarked_state_vs_oracle(gpu):
     rays = _torch_render(gpu, job, s, out)
     info = L.last_launch()
     assert info["kernel"] == "pool_kernel" and info["order"] == "2" and info["ns"] == "9", info
+    # a launch alone serves its lightest tiles as halves (the split tail, lrt_pool.h)
+    assert int(info["split_from"]) < int(info["tasks"]), info
     torch.cuda.synchronize()
     want, wrays = oracle.orc_render(w, h, 4, 8)
     _bitwise(out.cpu().numpy(), want, "config 2, order=2")
