@@ -654,7 +654,9 @@ def main():
     alone_ms = e2e_s = call_ms = None
     copy_ceiling = host_identical = None
     e2e_steps = 0
-    if extra:
+
+    def leg_end_to_end():
+        nonlocal host, copy_ceiling, host_identical, e2e_steps, e2e_s
         if rank == 0:
             # N = 1: the frame leaves as packed RGB (12 of the 16 B per pixel: the render never
             # writes alpha; lrt_pack_rgb on the render stream); N > 1: rank 0's assembled RGBA frame
@@ -698,6 +700,9 @@ def main():
                 dist.barrier()
         drain()
         sync_all()
+
+    def leg_alone():
+        nonlocal call_ms, alone_ms
         wd.enter("launch_alone")
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.steps)]
@@ -719,8 +724,15 @@ def main():
         # one render kernel per launch: the kernel's own events; else the call's
         alone_ms = sum(kt[:nk.value]) / nk.value if nk.value == args.steps else call_ms
 
+
+    # LRT_BENCH_LEGS (A/B of the order; default: both legs before the timed steps)
+    legs = os.environ.get("LRT_BENCH_LEGS", "e2e,alone,timed").split(",") if extra else ["timed"]
+    for leg in legs[:legs.index("timed")]:
+        {"e2e": leg_end_to_end, "alone": leg_alone}[leg]()
     elapsed, timed_rays = timed(mode)
     launch_info = L.last_launch()
+    for leg in legs[legs.index("timed") + 1:]:
+        {"e2e": leg_end_to_end, "alone": leg_alone}[leg]()
     exchange_legs = None
     if both and shared is None:   # the RCCL leg alone: the line still carries the exchange's timing
         wd.enter("exchange_legs")
