@@ -255,6 +255,23 @@ def test_libm_device_exhaustive_path_domain(gpu, manifest):
     del out
 
 
+def test_powf5_device_fast_path_domain(gpu):
+    """The device's powf5 (fast path + glibc fallback) on every float of [2^-14, 1] equals the
+    host build, which tests/test_libm.py checks against glibc on the same floats."""
+    import torch
+    from learnraytracing_amd import _lib as L
+    from test_libm import product
+    lo, hi, step = 0x38800000, 0x3F800000, 1 << 24
+    for a in range(lo, hi + 1, step):
+        x = np.arange(a, min(a + step, hi + 1), dtype=np.uint32).view(np.float32)
+        d_in = torch.from_numpy(x).cuda()
+        d_out = torch.empty_like(d_in)
+        L.check(L.lib().lrt_libm_eval_device(2, d_in.data_ptr(), d_out.data_ptr(), d_in.numel()))
+        got = d_out.cpu().numpy()
+        want = product(2, x)
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), hex(a)
+
+
 def test_fast_sqrt_rcp_correctly_rounded(gpu):
     """The device's short sqrt / reciprocal sequences (lrt_trace.h sqrt_rn, rcp_rn) equal
     IEEE sqrtf and 1/x bit for bit: every mantissa at exponents around the fast paths'

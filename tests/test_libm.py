@@ -78,6 +78,18 @@ def test_powf5_dense_and_edges(manifest):
     assert hashlib.sha256(product(2, pw).tobytes()).hexdigest() == manifest["libm"]["powf5_linspace01_2p20_sha256"]
 
 
+def test_powf5_fast_path_domain():
+    """powf5's fast path (lrt_libm.h: x^5 in double, returned when it lies farther than 2^-32
+    from a rounding boundary) over its whole domain, every float of [2^-14, 1] (117,440,513
+    inputs), against glibc's powf(x, 5): the fallback keeps every input where glibc does not round
+    correctly."""
+    lo, hi = 0x38800000, 0x3F800000
+    step = 1 << 24
+    for a in range(lo, hi + 1, step):
+        u = np.arange(a, min(a + step, hi + 1), dtype=np.uint32)
+        assert_same(2, u.view(np.float32))
+
+
 def test_powf_srgb_exponent():
     u = np.arange(0, np.float32(64.0).view(np.uint32), 67, dtype=np.uint32)
     assert_same(3, u.view(np.float32))
