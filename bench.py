@@ -532,6 +532,9 @@ def main():
     cstream = torch.cuda.Stream(device=dev)
     host = None   # pinned frame copies (end-to-end leg)
     e2e_rgb = []  # N = 1: the packed RGB frames the end-to-end leg copies
+    # N = 1, LRT_BENCH_E2E=fused (A/B): no copy -- the render's lerp stores each pixel (RGBA) straight
+    # into the pinned host frame over PCIe (lrt_render_device_to_frame)
+    e2e_fused = os.environ.get("LRT_BENCH_E2E", "copy") == "fused"
 
     def d2h_ceiling(src, dst, reps=10):
         """Pinned D2H bandwidth of this box (GB/s): reps copies of src into the page-locked dst
@@ -564,8 +567,9 @@ def main():
         if d2h and rank == 0:
             cstream.wait_event(done if done is not None else rdone)
             with torch.cuda.stream(cstream):
-                host[slot].copy_(frames_out[slot] if gather_ex else e2e_rgb[slot] if world == 1 else bufs[slot],
-                                 non_blocking=True)
+                if not (world == 1 and e2e_fused):
+                    host[slot].copy_(frames_out[slot] if gather_ex else e2e_rgb[slot] if world == 1 else bufs[slot],
+                                     non_blocking=True)
             done = torch.cuda.Event()
             done.record(cstream)
         if done is not None:   # the slot's next render waits for its gather / copy (step())
@@ -581,11 +585,14 @@ def main():
             rs.wait_event(prev)
         if mode == "remote":
             render_tensor_to_frame(job, bufs[slot], rays, shared.ptrs[slot], rs)
+        elif d2h and world == 1 and e2e_fused:   # the render's own stores land in pinned host memory
+            render_tensor_to_frame(job, bufs[slot], rays, host[slot].data_ptr(), rs)
         else:
             lrt.render_tensor(job, bufs[slot], rays, rs)
         rdone = None
         if d2h and world == 1:
-            pack_rgb_tensor(bufs[slot], e2e_rgb[slot], rs)
+            if not e2e_fused:
+                pack_rgb_tensor(bufs[slot], e2e_rgb[slot], rs)
             rdone = torch.cuda.Event()
             rdone.record(rs)
         work = None
@@ -660,7 +667,7 @@ def main():
         if rank == 0:
             # N = 1: the frame leaves as packed RGB (12 of the 16 B per pixel: the render never
             # writes alpha; lrt_pack_rgb on the render stream); N > 1: rank 0's assembled RGBA frame
-            shape = (H, W, 4) if world > 1 else tuple(bufs[0].shape[:2]) + (3,)   # --shard-of: the shard
+            shape = (H, W, 4) if world > 1 or e2e_fused else tuple(bufs[0].shape[:2]) + (3,)   # --shard-of: the shard
             host = [torch.empty(shape, dtype=torch.float32, pin_memory=True) for _ in range(e2e_slots)]
             if world == 1:
                 e2e_rgb[:] = [torch.empty(shape, dtype=torch.float32, device=dev) for _ in range(e2e_slots)]
@@ -694,7 +701,8 @@ def main():
             e2e_s = time.perf_counter() - t2
             if world == 1:   # the last frame on the host, bit for bit the device's RGB
                 last = (e2e_steps - 1) % e2e_slots
-                host_identical = bool(torch.equal(host[last].view(torch.int32),
+                hv = host[last][..., :3] if e2e_fused else host[last]
+                host_identical = bool(torch.equal(hv.contiguous().view(torch.int32),
                                                   bufs[last][..., :3].contiguous().cpu().view(torch.int32)))
             if world > 1:
                 dist.barrier()
