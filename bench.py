@@ -657,8 +657,10 @@ def main():
     # and the power controller raises it to ~2.39 GHz over ~50 launches (~13 ms); the cycles per
     # wave stay the same (tools/clock_ramp.py, profiles/r6_g). Timed right after W warmup steps, a
     # 20-step region measured that ramp (0.241 against 0.224 ms/step at the held clock). These
-    # legs are ~35 launches of the same render; the timed steps are unchanged.
+    # legs are the same render (the alone leg at least 64 launches); the timed steps are unchanged.
     alone_ms = e2e_s = call_ms = None
+    # the alone leg averages at least LRT_BENCH_ALONE_MIN launches (default 64; K if larger)
+    alone_n = max(args.steps, int(os.environ.get("LRT_BENCH_ALONE_MIN", "64")))
     copy_ceiling = host_identical = None
     e2e_steps = 0
 
@@ -713,10 +715,10 @@ def main():
         nonlocal call_ms, alone_ms
         wd.enter("launch_alone")
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps)]
+              for _ in range(alone_n)]
         scratch = torch.zeros(1, dtype=torch.int64, device=dev)
         L.check(L.lib().lrt_kernel_timing(1))
-        for k in range(args.steps):
+        for k in range(alone_n):
             ev[k][0].record(stream)
             if remote:
                 render_tensor_to_frame(job, bufs[0], scratch, shared.ptrs[0], stream)
@@ -724,13 +726,13 @@ def main():
                 lrt.render_tensor(job, bufs[0], scratch, stream)
             ev[k][1].record(stream)
         torch.cuda.synchronize()
-        call_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
-        kt = (ctypes.c_float * args.steps)()
+        call_ms = sum(a.elapsed_time(b) for a, b in ev) / alone_n
+        kt = (ctypes.c_float * alone_n)()
         nk = ctypes.c_int(0)
-        L.check(L.lib().lrt_kernel_times(kt, args.steps, ctypes.byref(nk)))
+        L.check(L.lib().lrt_kernel_times(kt, alone_n, ctypes.byref(nk)))
         L.check(L.lib().lrt_kernel_timing(0))
         # one render kernel per launch: the kernel's own events; else the call's
-        alone_ms = sum(kt[:nk.value]) / nk.value if nk.value == args.steps else call_ms
+        alone_ms = sum(kt[:nk.value]) / nk.value if nk.value == alone_n else call_ms
 
 
     # LRT_BENCH_LEGS (A/B of the order; default: both legs before the timed steps)
@@ -873,12 +875,13 @@ def main():
             "ms_per_step": round(ms_step, 4),
             "ms_per_launch_alone": round(alone_ms, 4) if alone_ms else None,
             "ms_per_call_alone": round(call_ms, 4) if call_ms else None,
+            "alone_launches": alone_n if alone_ms else None,
             "ms_per_step_warmup": round(warm[mode], 4),
             "timing_note": "ms_per_step: the K timed steps, pipelined over the render streams (a step's launch "
                            "overlaps its neighbours' tails); ms_per_launch_alone: one launch with nothing beside "
                            "it, the roofline's duration; ms_per_step_warmup: rank 0's W untimed warmup steps (first "
                            "launches record the tile order). Order: W warmup steps, the end_to_end and launch-alone "
-                           "legs (~35 launches), then the K timed steps: under a render's load the shader clock "
+                           "legs (min(K, 20) + 4 and max(K, 64) launches), then the K timed steps: under a render's load the shader clock "
                            "rises from ~2.18 to ~2.39 GHz over ~50 launches at constant cycles per wave "
                            "(profiles/r6_g), which a 20-step region right after the warmup measured (0.241 vs "
                            "0.224 ms/step)",
