@@ -457,7 +457,24 @@ __global__ __launch_bounds__(64 * kW, kWavesPerEU) void pool_kernel(
                     float4* const mpx = out + (size_t)my * xc + mx;
                     float4 acc = *mpx;
                     F3 c3 = f3(acc.x, acc.y, acc.z);
-                    for (int t = 0; t < nfr; ++t) {
+                    int t = 0;
+                    // four frames at a time: their colours and factors are read together (one
+                    // memory latency per four frames instead of one per frame), then chained in
+                    // frame order (config 2 -0.9 %, config 3 -1.0 %, profiles/r6_an)
+                    for (; t + 4 <= nfr; t += 4) {
+                        F3 c[4];
+                        float lf[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const float* const cp = slots + 3 * (((t + u) << lgP) + j);
+                            c[u] = f3(cp[0], cp[1], cp[2]);
+                            const int f = fr0 + t + u;
+                            lf[u] = f < kLerpTable ? lerp[f] : (float)f / (float)(f + 1);
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) c3 = c3 * lf[u] + c[u] * (1.0f - lf[u]);
+                    }
+                    for (; t < nfr; ++t) {
                         const float* const cp = slots + 3 * ((t << lgP) + j);
                         const F3 c = f3(cp[0], cp[1], cp[2]);
                         const int f = fr0 + t;
